@@ -1,0 +1,400 @@
+// C ABI of the ICRC engine (include/roce_icrc.h): contexts, host-buffer and
+// device-resident entry points, round-robin multi-GPU split.
+//
+// Every entry point that computes an ICRC runs the HIP kernels of
+// icrc_kernels.hip on the GPU; there is no host-side CRC in this library.
+#include "roce_icrc.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gf2.hpp"
+#include "icrc_internal.hpp"
+
+struct ricrc_ctx {
+  int device = -1;
+  int num_cus = 0;
+  int lanes = 0;  // 0 = automatic
+  hipStream_t stream = nullptr;
+  uint32_t* d_tables = nullptr;
+  // scratch for the host-buffer entry points
+  uint8_t* d_frames = nullptr;
+  size_t frames_cap = 0;
+  uint64_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  uint32_t* d_icrc = nullptr;
+  uint8_t* d_status = nullptr;
+  uint8_t* d_ok = nullptr;
+  size_t pkt_cap = 0;
+};
+
+namespace {
+
+std::once_flag g_prepare_once;
+
+int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? RICRC_ENOMEM : RICRC_EIO; }
+
+#define HIP_TRY(expr)                          \
+  do {                                         \
+    hipError_t _e = (expr);                    \
+    if (_e != hipSuccess) return hip_fail(_e); \
+  } while (0)
+
+int log2_lanes(int lanes) {
+  int l = 0;
+  while ((1 << l) < lanes) ++l;
+  return l;
+}
+
+// Lanes per packet: enough grid iterations per group to amortise the combine,
+// few enough that the front padding of the end-aligned grid stays small.
+int auto_log2g(uint32_t len) {
+  if (len < 8) return 0;
+  const uint32_t ndw = (len - 4) / 4;
+  int l = 0;
+  while (l < 4 && (ndw >> (l + 1)) >= 64) ++l;  // G = 16 at 4 KiB MTU, 1 at 64 B payloads
+  return l;
+}
+
+int pick_log2g(const ricrc_ctx* c, uint32_t typical_len) {
+  return c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(typical_len);
+}
+
+hipStream_t pick_stream(const ricrc_ctx* c, void* s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : c->stream;
+}
+
+int ensure_frames(ricrc_ctx* c, size_t bytes) {
+  if (bytes <= c->frames_cap) return RICRC_OK;
+  if (c->d_frames) (void)hipFree(c->d_frames);
+  c->d_frames = nullptr;
+  c->frames_cap = 0;
+  size_t cap = bytes < 4096 ? 4096 : bytes;
+  HIP_TRY(hipMalloc(&c->d_frames, cap));
+  c->frames_cap = cap;
+  return RICRC_OK;
+}
+
+int ensure_pkts(ricrc_ctx* c, size_t n) {
+  if (n <= c->pkt_cap) return RICRC_OK;
+  (void)hipFree(c->d_offs);
+  (void)hipFree(c->d_lens);
+  (void)hipFree(c->d_icrc);
+  (void)hipFree(c->d_status);
+  (void)hipFree(c->d_ok);
+  c->d_offs = nullptr;
+  c->d_lens = nullptr;
+  c->d_icrc = nullptr;
+  c->d_status = nullptr;
+  c->d_ok = nullptr;
+  c->pkt_cap = 0;
+  size_t cap = n < 1024 ? 1024 : n;
+  HIP_TRY(hipMalloc(&c->d_offs, cap * sizeof(uint64_t)));
+  HIP_TRY(hipMalloc(&c->d_lens, cap * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&c->d_icrc, cap * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&c->d_status, cap));
+  HIP_TRY(hipMalloc(&c->d_ok, cap));
+  c->pkt_cap = cap;
+  return RICRC_OK;
+}
+
+int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint32_t* lens,
+           uint64_t stride, uint32_t len, uint32_t n, uint32_t* icrc, uint8_t* status, uint8_t* ok,
+           bool ragged, bool verify, int log2g, hipStream_t s) {
+  ricrc::IcrcArgs a{};
+  a.frames = frames;
+  a.offsets = offs;
+  a.lens = lens;
+  a.stride = stride;
+  a.len = len;
+  a.n = n;
+  a.icrc_out = icrc;
+  a.status_out = status;
+  a.ok_out = ok;
+  a.tables = c->d_tables;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
+  return RICRC_OK;
+}
+
+// Mean frame length of a host length array (selects lanes per packet).
+uint32_t mean_len(const uint32_t* lens, uint32_t n) {
+  if (n == 0) return 0;
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < n; ++i) s += lens[i];
+  return (uint32_t)(s / n);
+}
+
+int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const uint64_t* offsets,
+                const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,
+                uint8_t* ok_out, bool verify) {
+  if (!c || (!frames && frames_bytes) || (n && (!offsets || !lens))) return RICRC_EINVAL;
+  if (verify ? !ok_out : !icrc_out) return RICRC_EINVAL;
+  if (n == 0) return RICRC_OK;
+  // every frame must lie inside the copied buffer
+  for (uint32_t i = 0; i < n; ++i)
+    if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = ensure_frames(c, frames_bytes);
+  if (rc) return rc;
+  rc = ensure_pkts(c, n);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_frames, frames, frames_bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_offs, offsets, n * sizeof(uint64_t), hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(
+      hipMemcpyAsync(c->d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  rc = launch(c, c->d_frames, c->d_offs, c->d_lens, 0, 0, n, c->d_icrc, c->d_status,
+              verify ? c->d_ok : nullptr, true, verify, pick_log2g(c, mean_len(lens, n)),
+              c->stream);
+  if (rc) return rc;
+  if (icrc_out)
+    HIP_TRY(hipMemcpyAsync(icrc_out, c->d_icrc, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           c->stream));
+  if (status_out)
+    HIP_TRY(hipMemcpyAsync(status_out, c->d_status, n, hipMemcpyDeviceToHost, c->stream));
+  if (verify) HIP_TRY(hipMemcpyAsync(ok_out, c->d_ok, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RICRC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ricrc_abi_version(void) { return RICRC_ABI_VERSION; }
+
+const char* ricrc_strerror(int code) {
+  switch (code) {
+    case RICRC_OK: return "ok";
+    case RICRC_EINVAL: return "invalid argument";
+    case RICRC_ENOMEM: return "out of memory";
+    case RICRC_ENODEV: return "no usable gfx950 device";
+    case RICRC_EIO: return "HIP runtime or kernel launch failure";
+    default: return "unknown error";
+  }
+}
+
+int ricrc_device_count(int* count) {
+  if (!count) return RICRC_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return RICRC_OK;
+}
+
+int ricrc_ctx_create(int device, ricrc_ctx** out) {
+  if (!out) return RICRC_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RICRC_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RICRC_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RICRC_ENODEV;
+  if (!ricrc::self_test()) return RICRC_EIO;
+  HIP_TRY(hipSetDevice(device));
+  hipError_t perr = hipSuccess;
+  std::call_once(g_prepare_once, [&] { perr = ricrc::prepare_kernels(); });
+  if (perr != hipSuccess) return hip_fail(perr);
+
+  ricrc_ctx* c = new (std::nothrow) ricrc_ctx();
+  if (!c) return RICRC_ENOMEM;
+  c->device = device;
+  c->num_cus = prop.multiProcessorCount;
+  std::vector<uint32_t> img(ricrc::kTableWords);
+  ricrc::build_table_image(img.data());
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->d_tables, img.size() * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = hipMemcpy(c->d_tables, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    ricrc_ctx_destroy(c);
+    return hip_fail(e);
+  }
+  *out = c;
+  return RICRC_OK;
+}
+
+void ricrc_ctx_destroy(ricrc_ctx* c) {
+  if (!c) return;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_tables);
+  (void)hipFree(c->d_frames);
+  (void)hipFree(c->d_offs);
+  (void)hipFree(c->d_lens);
+  (void)hipFree(c->d_icrc);
+  (void)hipFree(c->d_status);
+  (void)hipFree(c->d_ok);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int ricrc_ctx_set_lanes_per_packet(ricrc_ctx* c, int lanes) {
+  if (!c || lanes < 0 || lanes > 64 || (lanes & (lanes - 1))) return RICRC_EINVAL;
+  c->lanes = lanes;
+  return RICRC_OK;
+}
+
+void* ricrc_ctx_stream(ricrc_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int ricrc_lanes_for_len(ricrc_ctx* c, uint32_t len) {
+  if (!c) return RICRC_EINVAL;
+  return 1 << pick_log2g(c, len);
+}
+
+int ricrc_compute_one(ricrc_ctx* c, const uint8_t* frame, size_t len, uint32_t* icrc_out,
+                      uint8_t* status_out) {
+  if (!c || !frame || !icrc_out || len > 0xFFFFFFFFull) return RICRC_EINVAL;
+  const uint64_t off = 0;
+  const uint32_t l = (uint32_t)len;
+  return host_ragged(c, frame, len, &off, &l, 1, icrc_out, status_out, nullptr, false);
+}
+
+int ricrc_compute_batch(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,
+                        const uint64_t* offsets, const uint32_t* lens, uint32_t n,
+                        uint32_t* icrc_out, uint8_t* status_out) {
+  return host_ragged(c, frames, frames_bytes, offsets, lens, n, icrc_out, status_out, nullptr,
+                     false);
+}
+
+int ricrc_verify_batch(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,
+                       const uint64_t* offsets, const uint32_t* lens, uint32_t n, uint8_t* ok_out,
+                       uint32_t* icrc_out, uint8_t* status_out) {
+  return host_ragged(c, frames, frames_bytes, offsets, lens, n, icrc_out, status_out, ok_out,
+                     true);
+}
+
+int ricrc_compute_strided(ricrc_ctx* c, const uint8_t* frames, uint64_t stride, uint32_t len,
+                          uint32_t n, uint32_t* icrc_out, uint8_t* status_out) {
+  if (!c || !icrc_out || (n && !frames) || (n > 1 && stride < len)) return RICRC_EINVAL;
+  if (n == 0) return RICRC_OK;
+  const size_t bytes = (size_t)(n - 1) * stride + len;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = ensure_frames(c, bytes);
+  if (rc) return rc;
+  rc = ensure_pkts(c, n);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_frames, frames, bytes, hipMemcpyHostToDevice, c->stream));
+  rc = launch(c, c->d_frames, nullptr, nullptr, stride, len, n, c->d_icrc, c->d_status, nullptr,
+              false, false, pick_log2g(c, len), c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(icrc_out, c->d_icrc, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         c->stream));
+  if (status_out)
+    HIP_TRY(hipMemcpyAsync(status_out, c->d_status, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RICRC_OK;
+}
+
+int ricrc_compute_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
+                              size_t frames_bytes, const uint64_t* offsets, const uint32_t* lens,
+                              uint32_t n, uint32_t* icrc_out, uint8_t* status_out) {
+  if (!ctxs || nctx < 1 || !icrc_out || (n && (!frames || !offsets || !lens))) return RICRC_EINVAL;
+  for (int d = 0; d < nctx; ++d)
+    if (!ctxs[d]) return RICRC_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
+  std::vector<int> rcs(nctx, RICRC_OK);
+  std::vector<std::thread> th;
+  for (int d = 0; d < nctx; ++d) {
+    th.emplace_back([&, d] {
+      // gather packets d, d + nctx, ... into one contiguous host slice
+      std::vector<uint64_t> offs;
+      std::vector<uint32_t> ls;
+      size_t bytes = 0;
+      for (uint64_t i = d; i < n; i += nctx) {
+        offs.push_back(bytes);
+        ls.push_back(lens[i]);
+        bytes += (lens[i] + 3u) & ~3u;  // keep every frame dword aligned
+      }
+      const uint32_t m = (uint32_t)offs.size();
+      if (m == 0) return;
+      std::vector<uint8_t> buf;
+      std::vector<uint32_t> out(m);
+      std::vector<uint8_t> st(m);
+      try {
+        buf.resize(bytes);
+      } catch (...) {
+        rcs[d] = RICRC_ENOMEM;
+        return;
+      }
+      for (uint32_t k = 0; k < m; ++k)
+        std::memcpy(buf.data() + offs[k], frames + offsets[(uint64_t)k * nctx + d], ls[k]);
+      rcs[d] = ricrc_compute_batch(ctxs[d], buf.data(), bytes, offs.data(), ls.data(), m,
+                                   out.data(), st.data());
+      if (rcs[d]) return;
+      for (uint32_t k = 0; k < m; ++k) {
+        icrc_out[(uint64_t)k * nctx + d] = out[k];
+        if (status_out) status_out[(uint64_t)k * nctx + d] = st[k];
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int d = 0; d < nctx; ++d)
+    if (rcs[d]) return rcs[d];
+  return RICRC_OK;
+}
+
+int ricrc_host_register(void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return RICRC_EINVAL;
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return RICRC_OK;
+}
+
+int ricrc_host_unregister(void* ptr) {
+  if (!ptr) return RICRC_EINVAL;
+  HIP_TRY(hipHostUnregister(ptr));
+  return RICRC_OK;
+}
+
+int ricrc_compute_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_t* d_offsets,
+                            const uint32_t* d_lens, uint32_t n, uint32_t* d_icrc,
+                            uint8_t* d_status, void* stream) {
+  if (!c || !d_icrc || (n && (!d_frames || !d_offsets || !d_lens))) return RICRC_EINVAL;
+  // lanes per packet for ragged device batches: the context setting, else the
+  // 1 KiB-MTU choice (lengths are on the device; no host round trip)
+  return launch(c, d_frames, d_offsets, d_lens, 0, 0, n, d_icrc, d_status, nullptr, true, false,
+                pick_log2g(c, 1064 + 4), pick_stream(c, stream));
+}
+
+int ricrc_verify_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_t* d_offsets,
+                           const uint32_t* d_lens, uint32_t n, uint8_t* d_ok, uint32_t* d_icrc,
+                           uint8_t* d_status, void* stream) {
+  if (!c || !d_ok || (n && (!d_frames || !d_offsets || !d_lens))) return RICRC_EINVAL;
+  return launch(c, d_frames, d_offsets, d_lens, 0, 0, n, d_icrc, d_status, d_ok, true, true,
+                pick_log2g(c, 1064 + 4), pick_stream(c, stream));
+}
+
+int ricrc_compute_strided_dev(ricrc_ctx* c, const uint8_t* d_frames, uint64_t stride, uint32_t len,
+                              uint32_t n, uint32_t* d_icrc, uint8_t* d_status, void* stream) {
+  if (!c || !d_icrc || (n && !d_frames) || (n > 1 && stride < len)) return RICRC_EINVAL;
+  return launch(c, d_frames, nullptr, nullptr, stride, len, n, d_icrc, d_status, nullptr, false,
+                false, pick_log2g(c, len), pick_stream(c, stream));
+}
+
+int ricrc_verify_strided_dev(ricrc_ctx* c, const uint8_t* d_frames, uint64_t stride, uint32_t len,
+                             uint32_t n, uint8_t* d_ok, uint32_t* d_icrc, uint8_t* d_status,
+                             void* stream) {
+  if (!c || !d_ok || (n && !d_frames) || (n > 1 && stride < len)) return RICRC_EINVAL;
+  return launch(c, d_frames, nullptr, nullptr, stride, len, n, d_icrc, d_status, d_ok, false, true,
+                pick_log2g(c, len), pick_stream(c, stream));
+}
+
+int ricrc_stream_read_dev(ricrc_ctx* c, const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink,
+                          void* stream) {
+  if (!c || !d_buf || !d_sink || (bytes & 15)) return RICRC_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ricrc::launch_stream_read(d_buf, bytes, d_sink, c->num_cus, pick_stream(c, stream)));
+  return RICRC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,44 @@
+// Internal interface between the C ABI (icrc_capi.cpp) and the kernels
+// (icrc_kernels.hip).  Not installed; the public ABI is include/roce_icrc.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ricrc {
+
+// Device table image: 7 main sets (lanes-per-packet G = 1..64, log2 index) of
+// Mul(128 G), then the combine sets: [0] = Mul(-32), [1 + l] = Mul(-128 * 2^l).
+constexpr int kMaxLog2G = 6;
+constexpr int kNumMainSets = kMaxLog2G + 1;
+constexpr int kNumCombSets = kMaxLog2G + 1;
+constexpr int kTableWords = (kNumMainSets + kNumCombSets) * 1024;
+
+struct IcrcArgs {
+  const uint8_t* frames;
+  const uint64_t* offsets;  // ragged mode
+  const uint32_t* lens;     // ragged mode
+  uint64_t stride;          // strided mode
+  uint32_t len;             // strided mode
+  uint32_t n;
+  uint32_t* icrc_out;   // nullable
+  uint8_t* status_out;  // nullable
+  uint8_t* ok_out;      // verify mode
+  const uint32_t* tables;
+};
+
+// Builds the table image on the host (kTableWords words).
+void build_table_image(uint32_t* out);
+
+// Enqueues the ICRC kernel; returns a hipError_t.
+hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
+                       hipStream_t stream);
+
+// Enqueues the STREAM-style read kernel (roofline denominator).
+hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, int num_cus,
+                              hipStream_t stream);
+
+// Raises the dynamic-LDS limit of every kernel instantiation (once per device).
+hipError_t prepare_kernels();
+
+}  // namespace ricrc

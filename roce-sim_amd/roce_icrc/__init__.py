@@ -1,0 +1,18 @@
+"""MI355X-native RoCEv2 ICRC engine (drop-in for datenlord/roce-sim's
+BTH.compute_icrc, src/roce.py:192-223).
+
+Submodules:
+  engine  -- ctypes binding of libroceicrc.so (HIP kernels, C ABI)
+  roce    -- the reference's packet-object API (BTH, AETH, ... , IP, UDP)
+             with ICRC compute/verify routed through the engine
+  synth   -- synthetic frame batches for the BASELINE.json configurations
+"""
+
+from .engine import (  # noqa: F401
+    IcrcEngine,
+    IcrcError,
+    IcrcUnavailable,
+    compute_batch_multi,
+    load_library,
+    pack_icrc,
+)

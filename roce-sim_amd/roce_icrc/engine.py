@@ -1,0 +1,303 @@
+"""ctypes binding of ``libroceicrc.so`` (include/roce_icrc.h).
+
+This is the product path of the ICRC engine: every call below runs the HIP
+kernels on a gfx950 GPU.  There is deliberately no CPU fallback -- if the
+library or the GPU is missing, construction raises :class:`IcrcUnavailable`.
+
+Reference interface replaced: ``BTH.compute_icrc`` / ``BTH.pack_icrc``
+(datenlord/roce-sim src/roce.py:187-223), see include/roce_icrc.h for the
+mapping of every entry point.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+import numpy as np
+
+LIB_NAME = "libroceicrc.so"
+PKG_DIR = Path(__file__).resolve().parent
+REPO_ROOT = PKG_DIR.parent.parent
+HEADER = REPO_ROOT / "include" / "roce_icrc.h"
+
+RICRC_OK = 0
+PKT_BAD_LEN = 0x01
+PKT_NOT_IPV4 = 0x02
+PKT_NOT_UDP = 0x04
+PKT_LEN_MISMATCH = 0x08
+PKT_ICRC_MISMATCH = 0x10
+PKT_FATAL = PKT_BAD_LEN | PKT_NOT_IPV4 | PKT_NOT_UDP
+
+
+class IcrcUnavailable(RuntimeError):
+    """The HIP ICRC engine cannot run here (library not built, no gfx950 GPU)."""
+
+
+class IcrcError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed: {code} ({msg})")
+        self.code = code
+
+
+_c_u8p = ctypes.POINTER(ctypes.c_uint8)
+_c_u32p = ctypes.POINTER(ctypes.c_uint32)
+_c_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must cover every function in include/roce_icrc.h
+_SIGNATURES = {
+    "ricrc_abi_version": (ctypes.c_int, []),
+    "ricrc_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "ricrc_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "ricrc_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ricrc_ctx_destroy": (None, [_vp]),
+    "ricrc_ctx_set_lanes_per_packet": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "ricrc_ctx_stream": (_vp, [_vp]),
+    "ricrc_compute_one": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, _vp]),
+    "ricrc_compute_batch": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_uint32, _vp, _vp],
+    ),
+    "ricrc_verify_batch": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp],
+    ),
+    "ricrc_compute_strided": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp],
+    ),
+    "ricrc_compute_batch_multi": (
+        ctypes.c_int,
+        [_vp, ctypes.c_int, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_uint32, _vp, _vp],
+    ),
+    "ricrc_host_register": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "ricrc_host_unregister": (ctypes.c_int, [_vp]),
+    "ricrc_compute_batch_dev": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp],
+    ),
+    "ricrc_verify_batch_dev": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp],
+    ),
+    "ricrc_compute_strided_dev": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp],
+    ),
+    "ricrc_verify_strided_dev": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp],
+    ),
+    "ricrc_stream_read_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "ricrc_lanes_for_len": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+}
+
+_lib = None
+
+
+def library_path() -> Path:
+    return Path(os.environ.get("ROCE_ICRC_LIB", str(PKG_DIR / LIB_NAME)))
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libroceicrc.so and declare every exported signature.  Loading works
+    without a GPU (tests check the exports); computing needs one."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not path.exists():
+        raise IcrcUnavailable(
+            f"{path} is not built; run `make -C roce-sim_amd` (or __graft_entry__.build())"
+        )
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def header_functions(header: Path = HEADER) -> list[str]:
+    """Function names declared in include/roce_icrc.h."""
+    text = header.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ricrc_[a-z0-9_]+)\s*\(", text)))
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int(0)
+    lib.ricrc_device_count(ctypes.byref(n))
+    return n.value
+
+
+def _ptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags.c_contiguous:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):  # torch tensor (device-resident calls)
+        return a.data_ptr()
+    return int(a)
+
+
+def _u8(a) -> np.ndarray:
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(a, dtype=np.uint8)
+    a = np.ascontiguousarray(a)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8)
+    return a
+
+
+class IcrcEngine:
+    """One ICRC context on one GPU (one HIP stream).  Not thread-safe; use one
+    engine per thread, like the C context it wraps."""
+
+    def __init__(self, device: int = 0, lanes: int = 0):
+        self.lib = load_library()
+        if device_count() <= device:
+            raise IcrcUnavailable(f"no HIP device {device} visible")
+        ctx = _vp()
+        rc = self.lib.ricrc_ctx_create(device, ctypes.byref(ctx))
+        if rc != RICRC_OK or not ctx.value:
+            raise IcrcUnavailable(f"ricrc_ctx_create({device}) -> {rc} ({self._msg(rc)})")
+        self.ctx = ctx
+        self.device = device
+        if lanes:
+            self.set_lanes(lanes)
+
+    # -- plumbing ---------------------------------------------------------
+    def _msg(self, rc: int) -> str:
+        return self.lib.ricrc_strerror(rc).decode()
+
+    def _check(self, fn: str, rc: int) -> None:
+        if rc != RICRC_OK:
+            raise IcrcError(fn, rc, self._msg(rc))
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None) is not None and self.ctx.value:
+            self.lib.ricrc_ctx_destroy(self.ctx)
+            self.ctx = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_lanes(self, lanes: int) -> None:
+        self._check("ricrc_ctx_set_lanes_per_packet",
+                    self.lib.ricrc_ctx_set_lanes_per_packet(self.ctx, lanes))
+
+    def lanes_for_len(self, length: int) -> int:
+        return self.lib.ricrc_lanes_for_len(self.ctx, length)
+
+    @property
+    def stream(self) -> int:
+        return self.lib.ricrc_ctx_stream(self.ctx) or 0
+
+    # -- host buffers (synchronous) ----------------------------------------
+    def compute_one(self, frame) -> tuple[int, int]:
+        """Drop-in for BTH.compute_icrc (src/roce.py:192): wire frame -> (icrc, status)."""
+        f = _u8(frame)
+        out = np.zeros(1, np.uint32)
+        st = np.zeros(1, np.uint8)
+        self._check("ricrc_compute_one",
+                    self.lib.ricrc_compute_one(self.ctx, _ptr(f), f.size, _ptr(out), _ptr(st)))
+        return int(out[0]), int(st[0])
+
+    def compute_batch(self, frames, offsets, lens):
+        f = _u8(frames)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ls = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = offs.size
+        out = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.uint8)
+        self._check("ricrc_compute_batch", self.lib.ricrc_compute_batch(
+            self.ctx, _ptr(f), f.size, _ptr(offs), _ptr(ls), n, _ptr(out), _ptr(st)))
+        return out, st
+
+    def verify_batch(self, frames, offsets, lens):
+        f = _u8(frames)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ls = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = offs.size
+        ok = np.zeros(n, np.uint8)
+        out = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.uint8)
+        self._check("ricrc_verify_batch", self.lib.ricrc_verify_batch(
+            self.ctx, _ptr(f), f.size, _ptr(offs), _ptr(ls), n, _ptr(ok), _ptr(out), _ptr(st)))
+        return ok.astype(bool), out, st
+
+    def compute_strided(self, frames, stride: int, length: int, n: int):
+        f = _u8(frames)
+        if n and f.size < (n - 1) * stride + length:
+            raise ValueError("frames buffer too small")
+        out = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.uint8)
+        self._check("ricrc_compute_strided", self.lib.ricrc_compute_strided(
+            self.ctx, _ptr(f), stride, length, n, _ptr(out), _ptr(st)))
+        return out, st
+
+    # -- device-resident (torch CUDA tensors), asynchronous -----------------
+    def compute_strided_dev(self, d_frames, stride, length, n, d_icrc, d_status=None, stream=None):
+        self._check("ricrc_compute_strided_dev", self.lib.ricrc_compute_strided_dev(
+            self.ctx, _ptr(d_frames), stride, length, n, _ptr(d_icrc), _ptr(d_status), stream))
+
+    def verify_strided_dev(self, d_frames, stride, length, n, d_ok, d_icrc=None, d_status=None,
+                           stream=None):
+        self._check("ricrc_verify_strided_dev", self.lib.ricrc_verify_strided_dev(
+            self.ctx, _ptr(d_frames), stride, length, n, _ptr(d_ok), _ptr(d_icrc), _ptr(d_status),
+            stream))
+
+    def compute_batch_dev(self, d_frames, d_offsets, d_lens, n, d_icrc, d_status=None,
+                          stream=None):
+        self._check("ricrc_compute_batch_dev", self.lib.ricrc_compute_batch_dev(
+            self.ctx, _ptr(d_frames), _ptr(d_offsets), _ptr(d_lens), n, _ptr(d_icrc),
+            _ptr(d_status), stream))
+
+    def verify_batch_dev(self, d_frames, d_offsets, d_lens, n, d_ok, d_icrc=None, d_status=None,
+                         stream=None):
+        self._check("ricrc_verify_batch_dev", self.lib.ricrc_verify_batch_dev(
+            self.ctx, _ptr(d_frames), _ptr(d_offsets), _ptr(d_lens), n, _ptr(d_ok), _ptr(d_icrc),
+            _ptr(d_status), stream))
+
+    def stream_read_dev(self, d_buf, nbytes, d_sink, stream=None):
+        self._check("ricrc_stream_read_dev", self.lib.ricrc_stream_read_dev(
+            self.ctx, _ptr(d_buf), nbytes, _ptr(d_sink), stream))
+
+
+def compute_batch_multi(engines: list[IcrcEngine], frames, offsets, lens):
+    """Round-robin split over several GPUs (packet i -> engines[i % len])."""
+    lib = load_library()
+    f = _u8(frames)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ls = np.ascontiguousarray(lens, dtype=np.uint32)
+    n = offs.size
+    arr = (_vp * len(engines))(*[e.ctx.value for e in engines])
+    out = np.zeros(n, np.uint32)
+    st = np.zeros(n, np.uint8)
+    rc = lib.ricrc_compute_batch_multi(arr, len(engines), _ptr(f), f.size, _ptr(offs), _ptr(ls),
+                                       n, _ptr(out), _ptr(st))
+    if rc != RICRC_OK:
+        raise IcrcError("ricrc_compute_batch_multi", rc, lib.ricrc_strerror(rc).decode())
+    return out, st
+
+
+def pack_icrc(icrc: int) -> bytes:
+    """BTH.pack_icrc (src/roce.py:187-190): the wire bytes are little-endian."""
+    return int(icrc & 0xFFFFFFFF).to_bytes(4, "little")

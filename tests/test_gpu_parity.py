@@ -1,0 +1,271 @@
+"""GPU parity: the HIP ICRC engine (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact uint32 ICRC words for every frame.  The oracle restates
+BTH.compute_icrc (datenlord/roce-sim src/roce.py:192-223); see oracle/.
+"""
+import numpy as np
+import pytest
+
+from conftest import oracle_batch
+
+pytestmark = pytest.mark.gpu
+
+import icrc_oracle as o  # noqa: E402  (checker only)
+from roce_icrc import synth  # noqa: E402
+from roce_icrc.engine import (  # noqa: E402
+    PKT_BAD_LEN, PKT_ICRC_MISMATCH, PKT_LEN_MISMATCH, PKT_NOT_IPV4, PKT_NOT_UDP)
+
+LANES = [1, 2, 4, 8, 16, 32, 64]
+
+
+def _opcode_frames():
+    """One frame per (opcode shape, payload length) the simulator emits
+    (src/roce_sq.py:1243-1466, src/roce_rq.py:388-525, 767-854)."""
+    rng = np.random.default_rng(7)
+    frames = []
+    ext_for = {
+        0x00: b"", 0x01: b"", 0x02: b"", 0x04: b"",
+        0x03: o.immdt_bytes(0x1234), 0x05: o.immdt_bytes(0xBEEF),
+        0x06: o.reth_bytes(0x1000, 0x55, 4096), 0x07: b"", 0x08: b"",
+        0x09: o.immdt_bytes(7), 0x0A: o.reth_bytes(0x2000, 0x66, 100),
+        0x0B: o.reth_immdt_bytes(0x3000, 0x77, 10, 0x99),
+        0x0C: o.reth_bytes(0x4000, 0x88, 8192),
+        0x0D: o.aeth_bytes(0, 31, 5), 0x0E: b"", 0x0F: o.aeth_bytes(0, 31, 6),
+        0x10: o.aeth_bytes(0, 31, 7), 0x11: o.aeth_bytes(3, 2, 9),
+        0x12: o.aeth_bytes(0, 31, 3) + o.atomic_ack_eth_bytes(0x1122334455667788),
+        0x13: o.atomic_eth_bytes(0x5000, 0x1, 5, 6), 0x14: o.atomic_eth_bytes(0x6000, 0x2, 0, 9),
+        0x16: o.ieth_bytes(0xAB), 0x17: o.ieth_bytes(0xCD),
+        0x81: o.cnp_padding_bytes(),
+    }
+    no_payload = {0x0C, 0x11, 0x12, 0x13, 0x14, 0x81}
+    for op, ext in ext_for.items():
+        plens = [None] if op in no_payload else [0, 1, 2, 3, 4, 5, 255, 256, 1023, 4096]
+        for pl in plens:
+            payload = None if pl is None else rng.integers(0, 256, pl, dtype=np.uint8).tobytes()
+            frames.append(o.build_frame("192.168.0.1", "192.168.0.2", 0x33,
+                                        dict(opcode=op, psn=int(rng.integers(1 << 24)),
+                                             dqpn=0x11, ackreq=int(op & 1)),
+                                        ext=ext, payload=payload))
+    return frames
+
+
+def _pack(frames, align=4):
+    offs, pos = [], 0
+    for f in frames:
+        offs.append(pos)
+        pos += (len(f) + align - 1) // align * align
+    buf = np.zeros(pos, np.uint8)
+    for off, f in zip(offs, frames):
+        buf[off:off + len(f)] = np.frombuffer(f, np.uint8)
+    return buf, np.array(offs, np.uint64), np.array([len(f) for f in frames], np.uint32)
+
+
+def test_cfg1_sim_send_success(engine):
+    """Config 1: the sim_send_success SEND_ONLY; known value from SURVEY App. B."""
+    f = o.sim_send_success_frame()
+    icrc, st = engine.compute_one(f)
+    assert st == 0
+    assert icrc == 0x1BE21D75 == o.icrc_of_frame(f)
+    assert f[-4:] == bytes.fromhex("751de21b")
+
+
+@pytest.mark.parametrize("lanes", LANES)
+def test_every_opcode_shape(engine, lanes):
+    frames = _opcode_frames()
+    buf, offs, lens = _pack(frames)
+    engine.set_lanes(lanes)
+    try:
+        got, st = engine.compute_batch(buf, offs, lens)
+    finally:
+        engine.set_lanes(0)
+    want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
+    assert (st & 0x07 == 0).all()
+    np.testing.assert_array_equal(got, want)
+    ok, got2, _ = engine.verify_batch(buf, offs, lens)
+    assert ok.all()
+    np.testing.assert_array_equal(got2, want)
+
+
+@pytest.mark.parametrize("lanes", LANES)
+def test_uniform_4k_strided(engine, lanes):
+    n = 3000
+    buf, stride, flen = synth.uniform_frames(n, 4096, seed=synth.SEED_CFG2)
+    engine.set_lanes(lanes)
+    try:
+        got, st = engine.compute_strided(buf, stride, flen, n)
+    finally:
+        engine.set_lanes(0)
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("lanes", LANES)
+def test_mixed_mtu_compute_and_verify(engine, lanes):
+    n = 5000
+    buf, offs, lens = synth.mixed_mtu_frames(n, seed=synth.SEED_CFG3)
+    want, _ = oracle_batch(buf, offs, lens)
+    # fill trailers (little-endian ICRC) so verify has correct frames
+    for i in range(n):
+        e = int(offs[i] + lens[i])
+        buf[e - 4:e] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    rng = np.random.default_rng(3)
+    bad = rng.choice(n, 40, replace=False)
+    flip, masked = bad[:20], bad[20:]
+    for i in flip:  # payload bit flip: must fail
+        p = int(offs[i]) + 40 + int(rng.integers(0, lens[i] - 44))
+        buf[p] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    for i in masked:  # random values in masked fields: must still pass
+        b = int(offs[i])
+        for k in (1, 8, 10, 11, 26, 27, 32):
+            buf[b + k] = rng.integers(0, 256)
+    engine.set_lanes(lanes)
+    try:
+        got, st = engine.compute_batch(buf, offs, lens)
+        ok, got2, st2 = engine.verify_batch(buf, offs, lens)
+    finally:
+        engine.set_lanes(0)
+    want2, ok_want = oracle_batch(buf, offs, lens)
+    np.testing.assert_array_equal(got, want2)
+    np.testing.assert_array_equal(got2, want2)
+    np.testing.assert_array_equal(ok, ok_want.astype(bool))
+    assert not ok[flip].any()
+    assert ok[masked].all()
+    assert (st2[flip] & PKT_ICRC_MISMATCH).all()
+    assert ok.sum() == n - len(flip)
+
+
+def test_small_packets_cfg5_shape(engine):
+    n = 40000
+    buf, stride, flen = synth.uniform_frames(n, 64, seed=synth.SEED_CFG5)
+    got, st = engine.compute_strided(buf, stride, flen, n)
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_edge_cases_and_status(engine):
+    good = o.build_frame("1.2.3.4", "5.6.7.8", 9, dict(opcode=0x11, psn=5), ext=o.aeth_bytes())
+    bare = o.build_frame("1.2.3.4", "5.6.7.8", 9, dict(opcode=0x01, psn=5))  # 44 B minimum
+    assert len(bare) == 44
+    not_ip = b"\x60" + good[1:]          # IPv6 version nibble
+    not_udp = good[:9] + b"\x06" + good[10:]  # TCP protocol
+    short = good[:40]                    # shorter than IP+UDP+BTH+ICRC
+    odd = good + b"\0\0"                 # length not a multiple of 4
+    mism = good[:2] + b"\x00\x10" + good[4:]  # IP total length != frame length
+    # IPv4 with options (IHL 6): masks move with the UDP/BTH offsets
+    opt = bytearray(good[:20]) + b"\x01\x01\x01\x01" + good[20:]
+    opt[0] = 0x46
+    opt[2:4] = len(opt).to_bytes(2, "big")
+    opt = bytes(opt)
+    frames = [good, bare, not_ip, not_udp, short, odd, mism, opt]
+    buf, offs, lens = _pack(frames)
+    got, st = engine.compute_batch(buf, offs, lens)
+    assert got[0] == o.icrc_of_frame(good) and st[0] == 0
+    assert got[1] == o.icrc_of_frame(bare) and st[1] == 0
+    assert got[2] == 0 and st[2] & PKT_NOT_IPV4
+    assert got[3] == 0 and st[3] & PKT_NOT_UDP
+    assert got[4] == 0 and st[4] & PKT_BAD_LEN
+    assert got[5] == 0 and st[5] & PKT_BAD_LEN
+    assert got[6] == o.icrc_of_frame(mism) and st[6] == PKT_LEN_MISMATCH
+    assert got[7] == o.icrc_of_frame(opt) and st[7] == 0
+    # empty batch and single frame at the very end of the buffer
+    e0, s0 = engine.compute_batch(np.zeros(0, np.uint8), np.zeros(0, np.uint64),
+                                  np.zeros(0, np.uint32))
+    assert e0.size == 0
+    icrc, st1 = engine.compute_one(bare)
+    assert icrc == o.icrc_of_frame(bare)
+
+
+def test_unaligned_offsets(engine):
+    """Frames at every dword alignment modulo 16 and 128 bytes."""
+    rng = np.random.default_rng(11)
+    frames = [o.build_frame("10.0.0.1", "10.0.0.2", 3, dict(opcode=0x07, psn=i),
+                            payload=rng.integers(0, 256, int(rng.integers(0, 600)) * 4,
+                                                 dtype=np.uint8).tobytes())
+              for i in range(257)]
+    buf, offs, lens = _pack(frames, align=4)
+    assert len({int(x) % 16 for x in offs}) == 4
+    for lanes in (1, 16, 64):
+        engine.set_lanes(lanes)
+        got, _ = engine.compute_batch(buf, offs, lens)
+        np.testing.assert_array_equal(got, [o.icrc_of_frame(f) for f in frames])
+    engine.set_lanes(0)
+
+
+def test_mask_invariance_and_sensitivity(engine):
+    base = o.build_frame("10.9.8.7", "10.6.5.4", 17, dict(opcode=0x0A, psn=99, dqpn=0x42),
+                         ext=o.reth_bytes(1, 2, 3), payload=bytes(range(200)))
+    rng = np.random.default_rng(5)
+    variants = [base]
+    for _ in range(64):  # masked fields randomised: same ICRC
+        b = bytearray(base)
+        for k in (1, 8, 10, 11, 26, 27, 32):
+            b[k] = int(rng.integers(0, 256))
+        variants.append(bytes(b))
+    sens = []
+    for k in (4, 5, 6, 7, 30, 31, 36, 40, 100, len(base) - 5):  # id, flags, pkey, ackreq, data
+        b = bytearray(base)
+        b[k] ^= 0x01
+        sens.append(bytes(b))
+    buf, offs, lens = _pack(variants + sens)
+    got, _ = engine.compute_batch(buf, offs, lens)
+    ref = o.icrc_of_frame(base)
+    assert (got[:len(variants)] == ref).all()
+    assert (got[len(variants):] != ref).all()
+    np.testing.assert_array_equal(got[len(variants):], [o.icrc_of_frame(f) for f in sens])
+
+
+def test_device_resident_torch(engine):
+    torch = pytest.importorskip("torch")
+    n = 2048
+    buf, stride, flen = synth.uniform_frames(n, 4096, seed=1)
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.compute_strided_dev(d, stride, flen, n, out, st, stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    # write the trailers on the device, then verify there
+    rows = d.view(n, stride)
+    rows[:, flen - 4:flen] = out.view(torch.uint8).view(n, 4)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_strided_dev(d, stride, flen, n, ok, stream=s.cuda_stream)
+    s.synchronize()
+    assert bool(ok.all())
+    rows[7, 100] ^= 1
+    engine.verify_strided_dev(d, stride, flen, n, ok, stream=s.cuda_stream)
+    s.synchronize()
+    okc = ok.cpu().numpy()
+    assert okc[7] == 0 and okc.sum() == n - 1
+
+
+def test_multi_context_round_robin(engine):
+    from roce_icrc import IcrcEngine, compute_batch_multi
+    n = 3001
+    buf, offs, lens = synth.mixed_mtu_frames(n, seed=9)
+    e2 = IcrcEngine(0)
+    try:
+        got, _ = compute_batch_multi([engine, e2, e2], buf, offs, lens)
+    finally:
+        e2.close()
+    want, _ = oracle_batch(buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_full_size_cfg2_bit_exact(engine):
+    """BASELINE config 2 at full size (2^20 x 4 KiB frames): every ICRC word
+    against the multi-threaded C oracle."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 20
+    buf, stride, flen = synth.uniform_frames(n, 4096, seed=synth.SEED_CFG2)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.compute_strided_dev(d, stride, flen, n, out, stream=s.cuda_stream)
+    s.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    del d
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    np.testing.assert_array_equal(got, want)
