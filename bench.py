@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident RoCEv2 ICRC throughput on MI355X (BASELINE.json metric).
+
+One step = one launch of the HIP ICRC kernel over one batch of synthetic frames
+already resident in HBM.  Default workload (N=1): BASELINE config 2, 2^20 RC
+SEND_MIDDLE frames with 4 KiB payloads (4140-B wire frames, compute mode).
+With --gpus N (one process per GPU via torch.distributed.run) each rank owns its
+round-robin shard of 2^20 packets (BASELINE config 4 at N = 8: 2^23 packets in
+total); there is no data-path collective, only a gloo barrier and a max-reduce
+of the timing (weak scaling).
+
+Printed (rank 0): ONE JSON line with the driver's keys plus
+  roofline      -- achieved algorithmic GB/s of the ICRC kernel (per-launch
+                   bytes / mean launch time from HIP events on the launch
+                   stream) against the 8.0 TB/s HBM peak, and the PMC-measured
+                   HBM traffic per launch when profiles/pmc_traffic.json holds
+                   it for this workload;
+  cpu_baseline  -- the per-packet Python restatement of BTH.compute_icrc
+                   (datenlord/roce-sim src/roce.py:192-223, zlib.crc32), timed
+                   on this host's cores over a bounded sample (rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "roce-sim_amd"))
+
+METRIC = "ICRC GiB/s device-resident, 4 KiB MTU packets, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
+
+WORKLOADS = {
+    # name: (payload bytes, packets per GPU, seed, description)
+    "cfg2": (4096, 1 << 20, 0x1C2C0001,
+             "4 KiB-MTU RC SEND_MIDDLE frames (4140 B), ICRC compute, stride 4140"),
+    "cfg5": (64, 1 << 24, 0x1C2C0005,
+             "64-B payload SEND_MIDDLE-shaped frames (108 B), ICRC compute, stride 108"),
+}
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(buf: np.ndarray, stride: int, flen: int, n: int, gpu_icrc: np.ndarray):
+    """Per-packet zlib restatement (oracle/, the CPU "port" baseline) on this host.
+
+    Single process over the first n1 packets, then a fork pool over all n packets
+    (bounded: about 10 core-seconds).  Its CRCs double as a parity sample."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import multiprocessing as mp
+
+    import icrc_oracle as orc
+
+    cov = flen - 4
+    n1 = min(n, max(1, (1 << 28) // flen))  # ~256 MiB single-core sample
+    t0 = time.perf_counter()
+    one = np.array([orc.icrc_of_frame_at(buf, i * stride, flen) for i in range(n1)], np.uint32)
+    t1 = time.perf_counter() - t0
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    procs = max(1, min(16, cores))
+    global _CPU_JOB
+    _CPU_JOB = (buf, stride, flen)
+    chunks = [(s, min(n, s + (n + procs * 4 - 1) // (procs * 4)))
+              for s in range(0, n, (n + procs * 4 - 1) // (procs * 4))]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(procs) as pool:
+        parts = pool.map(_cpu_chunk, chunks)
+    tn = time.perf_counter() - t0
+    allc = np.concatenate(parts)
+    mism = int((allc != gpu_icrc[:n]).sum()) + int((one != gpu_icrc[:n1]).sum())
+    return {
+        "value": round(n * cov / tn / 2**30, 4),
+        "unit": "GiB/s",
+        "cores": procs,
+        "kind": "port",
+        "sample": (f"Python zlib.crc32 restatement of BTH.compute_icrc per packet over the same "
+                   f"host frames: {n} packets on a {procs}-process fork pool "
+                   f"({tn:.2f} s); single core {n1} packets {n1 * cov / t1 / 2**30:.3f} GiB/s"),
+        "single_core_GiBps": round(n1 * cov / t1 / 2**30, 4),
+        "parity_mismatches_vs_gpu": mism,
+    }
+
+
+_CPU_JOB = None
+
+
+def _cpu_chunk(se):
+    import icrc_oracle as orc
+    buf, stride, flen = _CPU_JOB
+    s, e = se
+    return np.array([orc.icrc_of_frame_at(buf, i * stride, flen) for i in range(s, e)], np.uint32)
+
+
+def main():
+    args = parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.gpus != world and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
+              file=sys.stderr)
+    torch.cuda.set_device(local)
+    from roce_icrc import IcrcEngine, synth
+
+    eng = IcrcEngine(local, lanes=args.lanes)
+    payload, n_default, seed, desc = WORKLOADS[args.workload]
+    n = args.packets or n_default
+    # rank r owns global packets r, r+N, r+2N, ... (round robin); its payloads
+    # come from its own PCG64 stream
+    buf, stride, flen = synth.uniform_frames(
+        n, payload, seed=seed if world == 1 else seed + rank, psn_start=rank, psn_step=world)
+    cov = flen - 4
+    dev = torch.device("cuda", local)
+    d_frames = torch.from_numpy(buf).to(dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        eng.compute_strided_dev(d_frames, stride, flen, n, out, stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    t_local = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kern_s = [a.elapsed_time(b) * 1e-3 for a, b in evs]
+    t = torch.tensor([t_local], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t[0])
+    gpu_icrc = out.cpu().numpy().view(np.uint32).copy()
+
+    # STREAM-style read of the same frame buffer (measured HBM-read denominator)
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    nb = d_frames.numel() // 16 * 16
+    eng.stream_read_dev(d_frames, nb, sink, stream=sp)
+    torch.cuda.synchronize(dev)
+    se = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    srs = []
+    for _ in range(5):
+        se[0].record(stream)
+        eng.stream_read_dev(d_frames, nb, sink, stream=sp)
+        se[1].record(stream)
+        se[1].synchronize()
+        srs.append(se[0].elapsed_time(se[1]) * 1e-3)
+    stream_read_gbps = nb / float(np.median(srs)) / 1e9
+
+    # host-inclusive rate: pinned H2D of the frames + kernel + D2H of the ICRCs
+    e2e = None
+    if not args.no_e2e:
+        h_pinned = torch.from_numpy(buf).pin_memory()
+        h_out = torch.empty(n, dtype=torch.int32).pin_memory()
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            d_frames.copy_(h_pinned, non_blocking=True)
+            step()
+            h_out.copy_(out, non_blocking=True)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        e2e = n * cov / min(ts) / 2**30
+        del h_pinned, h_out
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(buf, stride, flen, n, gpu_icrc)
+
+    if rank == 0:
+        mean_k = float(np.mean(kern_s))
+        alg_bytes = n * (cov + 4)  # C_i read + 4-B ICRC written
+        achieved = alg_bytes / mean_k / 1e9
+        traffic = None
+        if PMC_FILE.exists():
+            try:
+                pmc = json.loads(PMC_FILE.read_text())
+                if pmc.get("workload") == args.workload and pmc.get("packets") == n:
+                    traffic = pmc.get("traffic_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        value = world * n * cov / t_max / 2**30
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (numpy PCG64 payloads, scapy-default IPv4/UDP/BTH headers)",
+            "config": {
+                "workload": f"{args.workload}: {desc}",
+                "packets_per_gpu": n,
+                "frame_bytes": flen,
+                "covered_bytes_per_packet": cov,
+                "lanes_per_packet": eng.lanes_for_len(flen),
+                "parallelism": f"{world} GPU(s), round-robin packet shards, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+            },
+            "cpu_baseline": cpu,
+            "kernel_ms_mean": round(mean_k * 1e3, 4),
+            "stream_read_GBps": round(stream_read_gbps, 1),
+            "end_to_end_GiBps": None if e2e is None else round(e2e, 3),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -116,8 +116,9 @@ int ricrc_compute_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
 int ricrc_host_register(void* ptr, size_t bytes);
 int ricrc_host_unregister(void* ptr);
 
-/* ---- device-resident, asynchronous on `stream` (hipStream_t or NULL =
- *      the context's stream); all pointers are device pointers ------------ */
+/* ---- device-resident, asynchronous on `stream` (a hipStream_t; NULL is the
+ *      HIP null stream, as for any HIP API); all pointers are device
+ *      pointers ------------------------------------------------------------ */
 int ricrc_compute_batch_dev(ricrc_ctx* ctx, const uint8_t* d_frames, const uint64_t* d_offsets,
                             const uint32_t* d_lens, uint32_t n, uint32_t* d_icrc,
                             uint8_t* d_status /* nullable */, void* stream);

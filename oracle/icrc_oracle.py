@@ -97,6 +97,29 @@ def icrc_of_frame(frame: bytes) -> int:
     return zlib.crc32(m) & 0xFFFFFFFF
 
 
+_FF8_CRC = zlib.crc32(b"\xff" * 8)
+
+
+def icrc_of_frame_at(buf, off: int, length: int) -> int:
+    """Same rule as ``icrc_of_frame`` over ``buf[off:off+length]`` without
+    copying the payload: the masked header (IP/UDP/BTH) is re-built, the rest
+    is fed to zlib.crc32 as a memoryview (zlib's running-CRC argument).  This
+    is the per-packet CPU baseline ("port") timed by bench.py."""
+    mv = memoryview(buf)[off:off + length]
+    if length < 44 or (mv[0] >> 4) != 4:
+        return 0
+    ihl = mv[0] & 0x0F
+    hl = 4 * ihl + 8 + 12
+    if ihl < 5 or mv[9] != 17 or length < hl + 4:
+        return 0
+    h = bytearray(mv[:hl])
+    u = 4 * ihl
+    h[1] = h[8] = h[10] = h[11] = 0xFF
+    h[u + 6] = h[u + 7] = h[u + 12] = 0xFF
+    c = zlib.crc32(h, _FF8_CRC)
+    return zlib.crc32(mv[hl:length - 4], c) & 0xFFFFFFFF
+
+
 def icrc_bitwise(frame: bytes) -> int:
     """Independent check: reflected CRC-32 register seeded 0xDEBB20E3 (what the
     8 x 0xFF prefix leaves), bit by bit, no tables, no zlib.  Small inputs only."""

@@ -54,23 +54,28 @@ int log2_lanes(int lanes) {
   return l;
 }
 
-// Lanes per packet: enough grid iterations per group to amortise the combine,
-// few enough that the front padding of the end-aligned grid stays small.
+// Lanes per packet, measured on MI355X (profiles/): about 100 dwords
+// per lane keeps the group's combine cheap and the front padding of the
+// end-aligned grid small -> G = 8 at 4 KiB MTU, 4 at 1.5 KiB, 1 at 64-B payloads.
 int auto_log2g(uint32_t len) {
   if (len < 8) return 0;
-  const uint32_t ndw = (len - 4) / 4;
+  const uint32_t per = ((len - 4) / 4) / 100;
   int l = 0;
-  while (l < 4 && (ndw >> (l + 1)) >= 64) ++l;  // G = 16 at 4 KiB MTU, 1 at 64 B payloads
+  while (l < 4 && (2u << l) <= per) ++l;
   return l;
 }
+
+// Device-resident ragged batches: lengths live on the device, so the lane
+// count comes from the context setting or this typical length (the mean frame
+// of the BASELINE mixed-MTU configuration, 1632 B).
+constexpr uint32_t kRaggedTypicalLen = 1632;
 
 int pick_log2g(const ricrc_ctx* c, uint32_t typical_len) {
   return c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(typical_len);
 }
 
-hipStream_t pick_stream(const ricrc_ctx* c, void* s) {
-  return s ? reinterpret_cast<hipStream_t>(s) : c->stream;
-}
+// Device-resident calls run on the caller's stream; NULL is the HIP null stream.
+hipStream_t pick_stream(const ricrc_ctx*, void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 int ensure_frames(ricrc_ctx* c, size_t bytes) {
   if (bytes <= c->frames_cap) return RICRC_OK;
@@ -303,41 +308,56 @@ int ricrc_compute_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
     if (!ctxs[d]) return RICRC_EINVAL;
   for (uint32_t i = 0; i < n; ++i)
     if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
-  std::vector<int> rcs(nctx, RICRC_OK);
-  std::vector<std::thread> th;
+  // A context is single-threaded: shards that name the same context run one
+  // after another on that context's thread.
+  std::vector<ricrc_ctx*> uniq;
+  std::vector<std::vector<int>> shards_of;
   for (int d = 0; d < nctx; ++d) {
-    th.emplace_back([&, d] {
-      // gather packets d, d + nctx, ... into one contiguous host slice
-      std::vector<uint64_t> offs;
-      std::vector<uint32_t> ls;
-      size_t bytes = 0;
-      for (uint64_t i = d; i < n; i += nctx) {
-        offs.push_back(bytes);
-        ls.push_back(lens[i]);
-        bytes += (lens[i] + 3u) & ~3u;  // keep every frame dword aligned
-      }
-      const uint32_t m = (uint32_t)offs.size();
-      if (m == 0) return;
-      std::vector<uint8_t> buf;
-      std::vector<uint32_t> out(m);
-      std::vector<uint8_t> st(m);
-      try {
-        buf.resize(bytes);
-      } catch (...) {
-        rcs[d] = RICRC_ENOMEM;
-        return;
-      }
-      for (uint32_t k = 0; k < m; ++k)
-        std::memcpy(buf.data() + offs[k], frames + offsets[(uint64_t)k * nctx + d], ls[k]);
-      rcs[d] = ricrc_compute_batch(ctxs[d], buf.data(), bytes, offs.data(), ls.data(), m,
-                                   out.data(), st.data());
-      if (rcs[d]) return;
-      for (uint32_t k = 0; k < m; ++k) {
-        icrc_out[(uint64_t)k * nctx + d] = out[k];
-        if (status_out) status_out[(uint64_t)k * nctx + d] = st[k];
-      }
-    });
+    size_t u = 0;
+    while (u < uniq.size() && uniq[u] != ctxs[d]) ++u;
+    if (u == uniq.size()) {
+      uniq.push_back(ctxs[d]);
+      shards_of.emplace_back();
+    }
+    shards_of[u].push_back(d);
   }
+  std::vector<int> rcs(nctx, RICRC_OK);
+  auto run_shard = [&](int d) {
+    // gather packets d, d + nctx, ... into one contiguous host slice
+    std::vector<uint64_t> offs;
+    std::vector<uint32_t> ls;
+    size_t bytes = 0;
+    for (uint64_t i = d; i < n; i += nctx) {
+      offs.push_back(bytes);
+      ls.push_back(lens[i]);
+      bytes += (lens[i] + 3u) & ~3u;  // keep every frame dword aligned
+    }
+    const uint32_t m = (uint32_t)offs.size();
+    if (m == 0) return;
+    std::vector<uint8_t> buf;
+    std::vector<uint32_t> out(m);
+    std::vector<uint8_t> st(m);
+    try {
+      buf.resize(bytes);
+    } catch (...) {
+      rcs[d] = RICRC_ENOMEM;
+      return;
+    }
+    for (uint32_t k = 0; k < m; ++k)
+      std::memcpy(buf.data() + offs[k], frames + offsets[(uint64_t)k * nctx + d], ls[k]);
+    rcs[d] = ricrc_compute_batch(ctxs[d], buf.data(), bytes, offs.data(), ls.data(), m,
+                                 out.data(), st.data());
+    if (rcs[d]) return;
+    for (uint32_t k = 0; k < m; ++k) {
+      icrc_out[(uint64_t)k * nctx + d] = out[k];
+      if (status_out) status_out[(uint64_t)k * nctx + d] = st[k];
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t u = 0; u < uniq.size(); ++u)
+    th.emplace_back([&, u] {
+      for (int d : shards_of[u]) run_shard(d);
+    });
   for (auto& t : th) t.join();
   for (int d = 0; d < nctx; ++d)
     if (rcs[d]) return rcs[d];
@@ -363,7 +383,7 @@ int ricrc_compute_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_
   // lanes per packet for ragged device batches: the context setting, else the
   // 1 KiB-MTU choice (lengths are on the device; no host round trip)
   return launch(c, d_frames, d_offsets, d_lens, 0, 0, n, d_icrc, d_status, nullptr, true, false,
-                pick_log2g(c, 1064 + 4), pick_stream(c, stream));
+                pick_log2g(c, kRaggedTypicalLen), pick_stream(c, stream));
 }
 
 int ricrc_verify_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_t* d_offsets,
@@ -371,7 +391,7 @@ int ricrc_verify_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_t
                            uint8_t* d_status, void* stream) {
   if (!c || !d_ok || (n && (!d_frames || !d_offsets || !d_lens))) return RICRC_EINVAL;
   return launch(c, d_frames, d_offsets, d_lens, 0, 0, n, d_icrc, d_status, d_ok, true, true,
-                pick_log2g(c, 1064 + 4), pick_stream(c, stream));
+                pick_log2g(c, kRaggedTypicalLen), pick_stream(c, stream));
 }
 
 int ricrc_compute_strided_dev(ricrc_ctx* c, const uint8_t* d_frames, uint64_t stride, uint32_t len,

@@ -108,6 +108,13 @@ def load_library() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7).  Import
+    # it first so this library binds to that same HIP runtime: device pointers,
+    # streams and events are then shared with torch (one runtime per process).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     path = library_path()
     if not path.exists():
         raise IcrcUnavailable(

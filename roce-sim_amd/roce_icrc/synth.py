@@ -67,11 +67,13 @@ def _write_psn(hdr_rows: np.ndarray, psn: np.ndarray) -> None:
 
 
 def uniform_frames(n: int, payload_len: int = 4096, opcode: int = 0x01, seed: int = SEED_CFG2,
-                   psn_start: int = 0, chunk: int = 1 << 16) -> tuple[np.ndarray, int, int]:
+                   psn_start: int = 0, psn_step: int = 1,
+                   chunk: int = 1 << 16) -> tuple[np.ndarray, int, int]:
     """n back-to-back frames of identical length (cfg2/cfg4/cfg5).
 
     Returns (buffer, stride, frame_len) with stride == frame_len.  PSN of
-    packet i is (psn_start + i) mod 2^24."""
+    packet i is (psn_start + i * psn_step) mod 2^24 (psn_step = N for the
+    round-robin shard of rank psn_start out of N GPUs)."""
     assert payload_len % 4 == 0
     frame_len = HDR + payload_len + ICRC
     buf = np.empty(n * frame_len, dtype=np.uint8)
@@ -82,7 +84,7 @@ def uniform_frames(n: int, payload_len: int = 4096, opcode: int = 0x01, seed: in
         e = min(n, s + chunk)
         r = rows[s:e]
         r[:, :HDR] = tmpl
-        _write_psn(r, np.arange(psn_start + s, psn_start + e, dtype=np.int64))
+        _write_psn(r, psn_start + psn_step * np.arange(s, e, dtype=np.int64))
         r[:, HDR:HDR + payload_len] = _random_bytes(rng, (e - s) * payload_len).reshape(
             e - s, payload_len)
         r[:, HDR + payload_len:] = 0

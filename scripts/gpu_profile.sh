@@ -1,0 +1,29 @@
+# GPU session: parity tests, bench, rocprofv3 kernel-trace stats, PMC traffic passes.
+# usage: bash scripts/gpu_profile.sh <round tag, e.g. r01> [workload]
+set -u
+TAG=${1:-r01}
+WL=${2:-cfg2}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd $R
+make -C oracle -s || exit 1
+echo "== pytest -m gpu"
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_$TAG.log 2>&1
+rc=$?; tail -5 $OUT/pytest_$TAG.log; echo "pytest rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+echo "== bench"
+timeout -k 10 600 python bench.py --workload $WL > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+rc=$?; cat $OUT/bench_$TAG.json; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$TAG.err; exit $rc; }
+cd /tmp && export TMPDIR=/tmp
+echo "== rocprofv3 kernel trace"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > $OUT/prof_$TAG.log 2>&1
+rc=$?; tail -3 $OUT/prof_$TAG.log; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+echo "== pmc FETCH_SIZE"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmcf_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmcf_$TAG.log 2>&1
+rc=$?; tail -2 $OUT/pmcf_$TAG.log; echo "pmcf rc=$rc"; [ $rc -eq 0 ] || exit $rc
+echo "== pmc WRITE_SIZE"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcw_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmcw_$TAG.log 2>&1
+rc=$?; tail -2 $OUT/pmcw_$TAG.log; echo "pmcw rc=$rc"; [ $rc -eq 0 ] || exit $rc
+find $OUT/prof_$TAG $OUT/pmcf_$TAG -name "*.csv" | head
+exit 0
