@@ -219,7 +219,7 @@ def main():
                     traffic = pmc.get("traffic_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
-        value = world * n * cov / t_max / 2**30
+        value = world * n * cov * args.steps / t_max / 2**30
         line = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -54,12 +54,14 @@ int log2_lanes(int lanes) {
   return l;
 }
 
-// Lanes per packet, measured on MI355X (profiles/): about 100 dwords
-// per lane keeps the group's combine cheap and the front padding of the
-// end-aligned grid small -> G = 8 at 4 KiB MTU, 4 at 1.5 KiB, 1 at 64-B payloads.
+// Lanes per packet, measured on MI355X ("Lanes per packet"):
+// about 100 dwords per lane keeps the group's combine cheap while the group's
+// 16G-byte aligned runs stay long -> G = 8 at 4 KiB MTU, 4 at the mixed-MTU
+// mean (1.6 KiB), 2 for 64-B payloads.
 int auto_log2g(uint32_t len) {
-  if (len < 8) return 0;
+  if (len < 8) return 1;
   const uint32_t per = ((len - 4) / 4) / 100;
+  if (per == 0) return 1;
   int l = 0;
   while (l < 4 && (2u << l) <= per) ++l;
   return l;

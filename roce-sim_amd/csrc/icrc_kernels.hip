@@ -67,10 +67,11 @@ __device__ __forceinline__ void lds_wr4(uint32_t byte_addr, uint32_t v) {
 __device__ __forceinline__ uint32_t ldg32(const uint8_t* p) {
   return *(const uint32_t*)p;
 }
-// 16-byte load from a 4-byte-aligned address (frames are only dword aligned;
-// gfx950 runs global loads in unaligned mode).
+// 16-byte streaming load from a 4-byte-aligned address (frames are only dword
+// aligned; gfx950 runs global loads in unaligned mode).  Non-temporal: every
+// frame byte is read exactly once (measured +8-10 % HBM read rate on MI355X).
 __device__ __forceinline__ u32x4 ldg128(const uint8_t* p) {
-  return *(const u32x4*)p;
+  return __builtin_nontemporal_load((const u32x4*)p);
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -103,6 +104,161 @@ constexpr uint32_t kPktBadLen = 0x01, kPktNotIpv4 = 0x02, kPktNotUdp = 0x04,
                    kPktLenMismatch = 0x08, kPktIcrcMismatch = 0x10,
                    kPktFatal = kPktBadLen | kPktNotIpv4 | kPktNotUdp;
 
+// One packet as seen by its lane group, on the ALIGNED grid: iteration j
+// covers the absolute dwords [ab/4 + DPI j, ab/4 + DPI (j + 1)), so every lane
+// load is a 16-byte aligned chunk and every group run is 16G-byte aligned.
+struct Pkt {
+  const uint8_t* fp;  // frame start
+  const uint8_t* ab;  // frame start rounded down to a 4 DPI-byte boundary
+  uint32_t L;         // frame length incl. the ICRC slot
+  uint32_t pkt;       // index in the batch
+  int n;              // covered dwords (IP header .. last pad byte)
+  int S;              // grid column of the frame's first dword
+  int J;              // iterations
+  int r;              // valid columns in the last iteration (1 .. DPI)
+  int jh;             // iterations that may hold dwords k <= 8 (masks, seed, k < 0)
+  bool live;          // pkt < n: an output slot exists
+  bool dead;          // nothing to read: outside the batch or unusable length
+};
+
+template <int DPI>
+__device__ __forceinline__ Pkt describe(const uint8_t* frames, uint32_t pkt, bool live, uint64_t off,
+                                        uint32_t L) {
+  Pkt p;
+  p.fp = frames + off;
+  p.L = L;
+  p.pkt = pkt;
+  p.live = live;
+  p.dead = !live || L < 44 || (L & 3u) || L > 65535u;
+  p.S = (int)(((uintptr_t)p.fp >> 2) & (DPI - 1));
+  p.ab = p.fp - 4 * p.S;
+  p.n = p.dead ? 1 : (int)((L - 4) >> 2);
+  const int E = p.S + p.n;
+  p.J = (E + DPI - 1) / DPI;
+  p.r = E - DPI * (p.J - 1);
+  p.jh = (8 + p.S) / DPI + 1;
+  return p;
+}
+
+// The lane's 16-byte chunk of iteration j; chunks with no covered dword are
+// not loaded.  An aligned 4 DPI-byte block never crosses a page, so the bytes
+// around the frame that share its blocks are always mapped.
+template <int G>
+__device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
+  constexpr int DPI = 4 * G;
+  const int kb = DPI * j + 4 * gl - p.S;
+  u32x4 v = {0, 0, 0, 0};
+  if (!p.dead && kb + 3 >= 0 && kb < p.n) v = ldg128(p.ab + 16 * (G * j + gl));
+  return v;
+}
+
+// Masked dword k: TOS (k 0), TTL + IP checksum (k 2), UDP checksum (kub),
+// BTH fecn|becn|resv6 (kbb); the FF x 8 prefix enters as the register
+// 0xDEBB20E3 XORed into dword 0.
+__device__ __forceinline__ uint32_t fix_dword(uint32_t v, int k, int kub, int kbb) {
+  v |= (k == 0 ? 0x0000FF00u : 0u) | (k == 2 ? 0xFFFF00FFu : 0u) | (k == kub ? 0xFFFF0000u : 0u) |
+       (k == kbb ? 0x000000FFu : 0u);
+  return v ^ ((k == 0) ? kSeedRegister : 0u);
+}
+
+// Head fix-up of one chunk (iterations j < jh): zero dwords before the frame,
+// apply masks and seed, and keep the raw header dwords 0 and 2.
+__device__ __forceinline__ void fix_chunk(u32x4& w, int kb, int kub, int kbb, uint32_t& h0,
+                                          uint32_t& h2) {
+  h0 = (kb == 0) ? w.x : (kb == -1) ? w.y : (kb == -2) ? w.z : (kb == -3) ? w.w : h0;
+  h2 = (kb == 2) ? w.x : (kb == 1) ? w.y : (kb == 0) ? w.z : (kb == -1) ? w.w : h2;
+  w.x = (kb + 0 < 0) ? 0u : fix_dword(w.x, kb + 0, kub, kbb);
+  w.y = (kb + 1 < 0) ? 0u : fix_dword(w.y, kb + 1, kub, kbb);
+  w.z = (kb + 2 < 0) ? 0u : fix_dword(w.z, kb + 2, kub, kbb);
+  w.w = (kb + 3 < 0) ? 0u : fix_dword(w.w, kb + 3, kub, kbb);
+}
+
+// Fold the group's 4G column registers into the packet CRC register.  The
+// packet ends at column r of its last iteration, so column c is off by
+// x^(32 ((c - r) mod DPI)) (columns that skipped the last iteration are one
+// iteration early, which the modulus absorbs): rotate the columns by r
+// (in-lane select + ds_bpermute), then R = sum_c' Mul(-32 c')(V_c'), as
+// three in-lane Horner steps with Mul(-32) and log2 G butterfly levels with
+// Mul(-128 * 2^l).
+template <int LOG2G>
+__device__ __forceinline__ uint32_t combine(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                           int r, int gl, int base) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
+  const int rr = r & (DPI - 1);
+  const int q = rr >> 2, m = rr & 3;
+  const uint32_t v0 = m == 0 ? a0 : m == 1 ? a1 : m == 2 ? a2 : a3;
+  const uint32_t v1 = m == 0 ? a1 : m == 1 ? a2 : m == 2 ? a3 : a0;
+  const uint32_t v2 = m == 0 ? a2 : m == 1 ? a3 : m == 2 ? a0 : a1;
+  const uint32_t v3 = m == 0 ? a3 : m == 1 ? a0 : m == 2 ? a1 : a2;
+  uint32_t V0 = v0, V1 = v1, V2 = v2, V3 = v3;
+  if constexpr (G > 1) {
+    const int s0 = base + ((gl + q) & (G - 1));
+    const int s1 = base + ((gl + q + 1) & (G - 1));
+    V0 = (uint32_t)__shfl((int)v0, s0, 64);
+    V1 = (uint32_t)__shfl((int)v1, m >= 3 ? s1 : s0, 64);
+    V2 = (uint32_t)__shfl((int)v2, m >= 2 ? s1 : s0, 64);
+    V3 = (uint32_t)__shfl((int)v3, m >= 1 ? s1 : s0, 64);
+  }
+  uint32_t B = mul_comb(V3, kLdsMain) ^ V2;
+  B = mul_comb(B, kLdsMain) ^ V1;
+  B = mul_comb(B, kLdsMain) ^ V0;
+#pragma unroll
+  for (int l = 0; l < LOG2G; ++l) {
+    const uint32_t mm = mul_comb(B, kLdsMain + 4096u * (1 + l));
+    const uint32_t t = ((gl >> l) & 1) ? mm : B;
+    B = t ^ (uint32_t)__shfl_xor((int)t, 1 << l, 64);
+  }
+  return B;
+}
+
+// One iteration's fold; in the packet's last iteration, columns past the end
+// (k >= n) keep their register.
+__device__ __forceinline__ void fold(uint32_t (&A)[4], const u32x4& w, uint32_t kc0, uint32_t kc1) {
+#ifdef RICRC_ABLATE_FOLD  // diagnostic build only: loads kept, table folding removed
+  A[0] ^= w.x; A[1] ^= w.y; A[2] ^= w.z; A[3] ^= w.w;
+#else
+  A[0] = mul_main(A[0] ^ w.x, kc0, kc1);
+  A[1] = mul_main(A[1] ^ w.y, kc0, kc1);
+  A[2] = mul_main(A[2] ^ w.z, kc0, kc1);
+  A[3] = mul_main(A[3] ^ w.w, kc0, kc1);
+#endif
+}
+
+__device__ __forceinline__ void fold_last(uint32_t (&A)[4], const u32x4& w, int kb, int n,
+                                          uint32_t kc0, uint32_t kc1) {
+  const uint32_t f0 = mul_main(A[0] ^ w.x, kc0, kc1);
+  const uint32_t f1 = mul_main(A[1] ^ w.y, kc0, kc1);
+  const uint32_t f2 = mul_main(A[2] ^ w.z, kc0, kc1);
+  const uint32_t f3 = mul_main(A[3] ^ w.w, kc0, kc1);
+  A[0] = (kb + 0 < n) ? f0 : A[0];
+  A[1] = (kb + 1 < n) ? f1 : A[1];
+  A[2] = (kb + 2 < n) ? f2 : A[2];
+  A[3] = (kb + 3 < n) ? f3 : A[3];
+}
+
+// Recomputation of one packet by its group with the masks of a general IHL
+// (IPv4 options).  Rare path: the main loop applies the IHL-5 masks.
+template <int LOG2G>
+__device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, uint32_t kc0,
+                                             uint32_t kc1) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
+  const int kub = ihl + 1, kbb = ihl + 3;
+  uint32_t A[4] = {0, 0, 0, 0};
+  uint32_t h0 = 0, h2 = 0;
+  for (int j = 0; j < p.J; ++j) {
+    const int kb = DPI * j + 4 * gl - p.S;
+    u32x4 w = load_chunk<G>(p, j, gl);
+    fix_chunk(w, kb, kub, kbb, h0, h2);
+    if (j == p.J - 1)
+      fold_last(A, w, kb, p.n, kc0, kc1);
+    else
+      fold(A, w, kc0, kc1);
+  }
+  return combine<LOG2G>(A[0], A[1], A[2], A[3], p.r, gl, base);
+}
+
 template <int LOG2G, bool RAGGED, bool VERIFY>
 __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
@@ -130,13 +286,18 @@ __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
   const int grp = lane >> LOG2G;
+  const int base = grp * G;
   const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
   const uint32_t kc1 = kc0 | 0x10000u;
+  // Each workgroup owns a contiguous range of packet sets, so every CU sweeps
+  // one contiguous region of HBM (measured: 6.8 vs 5.6 TB/s for
+  // grid-interleaved sets); its 16 waves take consecutive sets of that range.
   const uint32_t nsets = (a.n + PPW - 1) / PPW;
-  const uint32_t wave = blockIdx.x * 16u + (uint32_t)(tid >> 6);
-  const uint32_t nwaves = gridDim.x * 16u;
+  const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
+  const uint32_t set_begin = blockIdx.x * per_block;
+  const uint32_t set_end = min(nsets, set_begin + per_block);
 
-  for (uint32_t set = wave; set < nsets; set += nwaves) {
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
     const uint32_t pkt = set * PPW + grp;
     const bool live = pkt < a.n;
     uint64_t off = 0;
@@ -150,97 +311,78 @@ __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
         L = a.len;
       }
     }
-    const uint8_t* fp = a.frames + off;
+    const Pkt p = describe<DPI>(a.frames, pkt, live, off, L);
 
-    // ---- frame checks (reference warning path -> ICRC 0) --------------------
-    uint32_t st = (!live || L < 44 || (L & 3u) || L > 65535u) ? kPktBadLen : 0u;
-    uint32_t d0 = 0, d2 = 0;
-    if (st == 0) {
-      d0 = ldg32(fp);
-      d2 = ldg32(fp + 8);
+    // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
+    // U (the first block holds the remainder), then the last one (J-1), which
+    // skips columns past the end and may also need the fix-ups.  The head
+    // chunks, the first body block and the last chunk are issued together.
+    const int JL = p.J - 1;
+    const int jhh = min(p.jh, JL);
+    const int nbody = JL - jhh;
+    const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
+    const int nblk = (nbody + U - 1) / U;
+    uint32_t trailer = 0;
+    if (VERIFY && !p.dead && gl == 0) trailer = ldg32(p.fp + p.L - 4);
+    const u32x4 wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
+    const u32x4 wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
+    u32x4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      cur[u] = u < first ? load_chunk<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
+    const u32x4 wl = load_chunk<G>(p, JL, gl);
+
+    uint32_t A[4] = {0, 0, 0, 0};
+    uint32_t h0 = 0, h2 = 0;
+    for (int j = 0; j < jhh; ++j) {
+      u32x4 w = (j == 0) ? wh0 : (j == 1) ? wh1 : load_chunk<G>(p, j, gl);
+      fix_chunk(w, DPI * j + 4 * gl - p.S, 6, 8, h0, h2);
+      fold(A, w, kc0, kc1);
     }
+    int j0 = jhh, bs = first;
+    for (int b = 0; b < nblk; ++b) {
+      u32x4 nxt[U];
+      const int jn = j0 + bs;
+      if (b + 1 < nblk) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = load_chunk<G>(p, jn + u, gl);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < bs) fold(A, cur[u], kc0, kc1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+      j0 = jn;
+      bs = U;
+    }
+    {
+      u32x4 w = wl;
+      const int kb = DPI * JL + 4 * gl - p.S;
+      if (JL < p.jh) fix_chunk(w, kb, 6, 8, h0, h2);
+      fold_last(A, w, kb, p.n, kc0, kc1);
+    }
+
+    // ---- packet done: fold the group, check the header, emit ----------------
+    uint32_t B = combine<LOG2G>(A[0], A[1], A[2], A[3], p.r, gl, base);
+    const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
+    const uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
+    uint32_t st = p.dead ? kPktBadLen : 0u;
     const int ihl = (int)(d0 & 0xFu);
     if (st == 0) {
       if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
         st |= kPktNotIpv4;
       else if (((d2 >> 8) & 0xFFu) != 17u)
         st |= kPktNotUdp;
-      else if (L < (uint32_t)(4 * ihl + 24))
+      else if (p.L < (uint32_t)(4 * ihl + 24))
         st |= kPktBadLen;
       const uint32_t tot = ((d0 >> 8) & 0xFF00u) | (d0 >> 24);
-      if (tot != L) st |= kPktLenMismatch;
+      if (tot != p.L) st |= kPktLenMismatch;
     }
     const bool good = (st & kPktFatal) == 0;
-    const int ndw = good ? (int)((L - 4) >> 2) : 0;
-    const int J = (ndw + DPI - 1) / DPI;
-    const int pad = J * DPI - ndw;
-    const int kub = ihl + 1;  // UDP checksum dword
-    const int kbb = ihl + 3;  // BTH fecn|becn|resv6 dword
-    int JH = min(J, (kbb + pad) / DPI + 1);
-    JH = J - ((J - JH) / U) * U;  // body = whole blocks of U iterations
-
-    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-
-    // ---- head: front padding, masks and seed --------------------------------
-    for (int j = 0; j < JH; ++j) {
-      const int kb = DPI * j + 4 * gl - pad;
-      uint32_t w[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int k = kb + t;
-        uint32_t v = 0;
-        if (k >= 0) v = ldg32(fp + 4 * k);
-        v |= (k == 0 ? 0x0000FF00u : 0u) | (k == 2 ? 0xFFFF00FFu : 0u) |
-             (k == kub ? 0xFFFF0000u : 0u) | (k == kbb ? 0x000000FFu : 0u);
-        v ^= (k == 0) ? kSeedRegister : 0u;
-        w[t] = v;
-      }
-      a0 = mul_main(a0 ^ w[0], kc0, kc1);
-      a1 = mul_main(a1 ^ w[1], kc0, kc1);
-      a2 = mul_main(a2 ^ w[2], kc0, kc1);
-      a3 = mul_main(a3 ^ w[3], kc0, kc1);
-    }
-
-    // ---- body: blocks of U iterations, next block's loads in flight ---------
-    const int nb = (J - JH) / U;
-    const uint8_t* bp = fp + 4 * (int64_t)(DPI * JH + 4 * gl - pad);
-    u32x4 cur[U];
-    if (nb > 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = ldg128(bp + 16 * G * u);
-    }
-    for (int b = 0; b < nb; ++b) {
-      u32x4 nxt[U];
-      if (b + 1 < nb) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) nxt[u] = ldg128(bp + 16 * G * (U * (b + 1) + u));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        a0 = mul_main(a0 ^ cur[u].x, kc0, kc1);
-        a1 = mul_main(a1 ^ cur[u].y, kc0, kc1);
-        a2 = mul_main(a2 ^ cur[u].z, kc0, kc1);
-        a3 = mul_main(a3 ^ cur[u].w, kc0, kc1);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-    }
-
-    // ---- combine: in-lane Horner, then butterfly across the group -----------
-    uint32_t B = mul_comb(a3, kLdsMain) ^ a2;
-    B = mul_comb(B, kLdsMain) ^ a1;
-    B = mul_comb(B, kLdsMain) ^ a0;
-#pragma unroll
-    for (int l = 0; l < LOG2G; ++l) {
-      const uint32_t m = mul_comb(B, kLdsMain + 4096u * (1 + l));
-      const uint32_t t = ((gl >> l) & 1) ? m : B;
-      B = t ^ (uint32_t)__shfl_xor((int)t, 1 << l, 64);
-    }
+    if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kc0, kc1);
     const uint32_t icrc = good ? ~B : 0u;
-
     if (live && gl == 0) {
       if constexpr (VERIFY) {
-        const uint32_t trailer = good ? ldg32(fp + L - 4) : 0u;
         const bool ok = good && trailer == icrc;
         if (good && !ok) st |= kPktIcrcMismatch;
         a.ok_out[pkt] = ok ? 1 : 0;
@@ -251,20 +393,24 @@ __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(256) stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
-                                                          uint32_t* sink) {
+// STREAM-style read ceiling with the same geometry as the ICRC kernel: one
+// 1024-thread workgroup per CU sweeping a contiguous chunk, 16-B nt loads.
+__global__ void __launch_bounds__(1024) stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                           uint32_t* sink) {
   constexpr int R = 8;
-  const uint64_t gsz = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per;
+  const uint64_t b1 = b0 + per < n16 ? b0 + per : n16;
   u32x4 acc = {0, 0, 0, 0};
-  for (; i + (R - 1) * gsz < n16; i += R * gsz) {
+  uint64_t i = b0 + threadIdx.x;
+  for (; i + (R - 1) * 1024 < b1; i += R * 1024) {
     u32x4 v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = p[i + r * gsz];
+    for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load(p + i + r * 1024);
 #pragma unroll
     for (int r = 0; r < R; ++r) acc ^= v[r];
   }
-  for (; i < n16; i += gsz) acc ^= p[i];
+  for (; i < b1; i += 1024) acc ^= p[i];
   const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
   if (x == 0x9E3779B9u) sink[0] = x;  // keeps the loads live; practically never stores
 }
@@ -332,7 +478,7 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink
                               hipStream_t stream) {
   const uint64_t n16 = bytes / 16;
   if (n16 == 0) return hipSuccess;
-  hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)(num_cus * 8)), dim3(256), 0, stream,
+  hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)num_cus), dim3(1024), 0, stream,
                      (const u32x4*)buf, n16, sink);
   return hipGetLastError();
 }
