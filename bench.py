@@ -49,8 +49,10 @@ WORKLOADS = {
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults: the chip's power management settles within ~30 back-to-back
+    # launches (profiles/, DESIGN.md "Measurement"); 100 timed launches ~ 70 ms
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")

@@ -52,7 +52,10 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 constexpr uint32_t kLdsMain = 131072;
-constexpr int kUnroll = 4;  // iterations per body block (dwordx4 loads in flight per lane)
+#ifndef RICRC_UNROLL
+#define RICRC_UNROLL 4
+#endif
+constexpr int kUnroll = RICRC_UNROLL;  // iterations per body block (dwordx4 loads in flight per lane)
 
 __device__ __forceinline__ uint32_t lds_rd(uint32_t byte_addr) {
   return *(const lds_u32*)(uintptr_t)byte_addr;
@@ -76,19 +79,6 @@ __device__ __forceinline__ u32x4 ldg128(const uint8_t* p) {
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// Mul(128 G)(x) from the replicated LDS tables.
-__device__ __forceinline__ uint32_t mul_main(uint32_t x, uint32_t kc0, uint32_t kc1) {
-  const uint32_t a0 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(x, kc1, 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(x, kc1, 0x0C020700u);
-  const uint32_t t0 = lds_rd(a0);
-  const uint32_t t1 = lds_rd(a1 + 128);
-  const uint32_t t2 = lds_rd(a2);
-  const uint32_t t3 = lds_rd(a3 + 128);
-  return xor3(t0, t1, t2) ^ t3;
 }
 
 // Mul(m)(x) from an unreplicated combine set at LDS byte address `base`.
@@ -152,6 +142,12 @@ __device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
   return v;
 }
 
+// Body iterations (jh <= j < J-1) lie wholly inside the frame: no predicate.
+template <int G>
+__device__ __forceinline__ u32x4 load_body(const Pkt& p, int j, int gl) {
+  return ldg128(p.ab + 16 * (G * j + gl));
+}
+
 // Masked dword k: TOS (k 0), TTL + IP checksum (k 2), UDP checksum (kub),
 // BTH fecn|becn|resv6 (kbb); the FF x 8 prefix enters as the register
 // 0xDEBB20E3 XORed into dword 0.
@@ -212,29 +208,46 @@ __device__ __forceinline__ uint32_t combine(uint32_t a0, uint32_t a1, uint32_t a
   return B;
 }
 
-// One iteration's fold; in the packet's last iteration, columns past the end
-// (k >= n) keep their register.
-__device__ __forceinline__ void fold(uint32_t (&A)[4], const u32x4& w, uint32_t kc0, uint32_t kc1) {
+// Column registers are kept as a pair (P, T) whose XOR is the CRC register:
+// P = t0 ^ t1 ^ t2 and T = t3 of the last four lookups.  Absorbing the next
+// dword is then ONE v_bitop3 (P ^ T ^ w), four v_perm address builds, four
+// conflict-free ds_read_b32 and one more v_bitop3: 6 VALU per dword.
+struct Col {
+  uint32_t P[4], T[4];
+};
+
+__device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w, uint32_t kc0,
+                                       uint32_t kc1) {
 #ifdef RICRC_ABLATE_FOLD  // diagnostic build only: loads kept, table folding removed
-  A[0] ^= w.x; A[1] ^= w.y; A[2] ^= w.z; A[3] ^= w.w;
+  P ^= w;
 #else
-  A[0] = mul_main(A[0] ^ w.x, kc0, kc1);
-  A[1] = mul_main(A[1] ^ w.y, kc0, kc1);
-  A[2] = mul_main(A[2] ^ w.z, kc0, kc1);
-  A[3] = mul_main(A[3] ^ w.w, kc0, kc1);
+  const uint32_t x = xor3(P, T, w);
+  const uint32_t a0 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, kc1, 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, kc1, 0x0C020700u);
+  P = xor3(lds_rd(a0), lds_rd(a1 + 128), lds_rd(a2));
+  T = lds_rd(a3 + 128);
 #endif
 }
 
-__device__ __forceinline__ void fold_last(uint32_t (&A)[4], const u32x4& w, int kb, int n,
-                                          uint32_t kc0, uint32_t kc1) {
-  const uint32_t f0 = mul_main(A[0] ^ w.x, kc0, kc1);
-  const uint32_t f1 = mul_main(A[1] ^ w.y, kc0, kc1);
-  const uint32_t f2 = mul_main(A[2] ^ w.z, kc0, kc1);
-  const uint32_t f3 = mul_main(A[3] ^ w.w, kc0, kc1);
-  A[0] = (kb + 0 < n) ? f0 : A[0];
-  A[1] = (kb + 1 < n) ? f1 : A[1];
-  A[2] = (kb + 2 < n) ? f2 : A[2];
-  A[3] = (kb + 3 < n) ? f3 : A[3];
+__device__ __forceinline__ void fold(Col& c, const u32x4& w, uint32_t kc0, uint32_t kc1) {
+  absorb(c.P[0], c.T[0], w.x, kc0, kc1);
+  absorb(c.P[1], c.T[1], w.y, kc0, kc1);
+  absorb(c.P[2], c.T[2], w.z, kc0, kc1);
+  absorb(c.P[3], c.T[3], w.w, kc0, kc1);
+}
+
+// The packet's last iteration: columns past the end (k >= n) keep their register.
+__device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n, uint32_t kc0,
+                                          uint32_t kc1) {
+  Col f = c;
+  fold(f, w, kc0, kc1);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    c.P[t] = (kb + t < n) ? f.P[t] : c.P[t];
+    c.T[t] = (kb + t < n) ? f.T[t] : c.T[t];
+  }
 }
 
 // Recomputation of one packet by its group with the masks of a general IHL
@@ -245,7 +258,7 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, u
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   const int kub = ihl + 1, kbb = ihl + 3;
-  uint32_t A[4] = {0, 0, 0, 0};
+  Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < p.J; ++j) {
     const int kb = DPI * j + 4 * gl - p.S;
@@ -256,7 +269,8 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, u
     else
       fold(A, w, kc0, kc1);
   }
-  return combine<LOG2G>(A[0], A[1], A[2], A[3], p.r, gl, base);
+  return combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2], A.P[3] ^ A.T[3], p.r,
+                        gl, base);
 }
 
 template <int LOG2G, bool RAGGED, bool VERIFY>
@@ -329,29 +343,37 @@ __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
     u32x4 cur[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      cur[u] = u < first ? load_chunk<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
+      cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
     const u32x4 wl = load_chunk<G>(p, JL, gl);
 
-    uint32_t A[4] = {0, 0, 0, 0};
+    Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     uint32_t h0 = 0, h2 = 0;
     for (int j = 0; j < jhh; ++j) {
       u32x4 w = (j == 0) ? wh0 : (j == 1) ? wh1 : load_chunk<G>(p, j, gl);
       fix_chunk(w, DPI * j + 4 * gl - p.S, 6, 8, h0, h2);
       fold(A, w, kc0, kc1);
     }
+    // body blocks, ping-pong between cur and nxt (no register copies)
     int j0 = jhh, bs = first;
-    for (int b = 0; b < nblk; ++b) {
-      u32x4 nxt[U];
-      const int jn = j0 + bs;
+    u32x4 nxt[U];
+    for (int b = 0; b < nblk; b += 2) {
+      int jn = j0 + bs;
       if (b + 1 < nblk) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) nxt[u] = load_chunk<G>(p, jn + u, gl);
+        for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (u < bs) fold(A, cur[u], kc0, kc1);
+      if (b + 1 >= nblk) break;
+      j0 = jn;
+      jn = j0 + U;
+      if (b + 2 < nblk) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < U; ++u) cur[u] = load_body<G>(p, jn + u, gl);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) fold(A, nxt[u], kc0, kc1);
       j0 = jn;
       bs = U;
     }
@@ -363,7 +385,8 @@ __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
     }
 
     // ---- packet done: fold the group, check the header, emit ----------------
-    uint32_t B = combine<LOG2G>(A[0], A[1], A[2], A[3], p.r, gl, base);
+    uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                A.P[3] ^ A.T[3], p.r, gl, base);
     const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
     const uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
     uint32_t st = p.dead ? kPktBadLen : 0u;

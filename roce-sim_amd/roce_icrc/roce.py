@@ -1,0 +1,571 @@
+"""RoCEv2 packet objects with the reference's API, ICRC through the HIP engine.
+
+Mirrors the layer classes of datenlord/roce-sim ``src/roce.py`` (a scapy
+contrib fork) without scapy: ``BTH`` (src/roce.py:168-233), the extension
+headers ``AETH``/``RETH``/``AtomicETH``/``AtomicAckETH``/``ImmDt``/``IETH``/
+``RETHImmDt``/``CNPPadding``/``GRH`` (src/roce.py:236-321), the opcode table
+(src/roce.py:34-165), ``cnp()`` and the ``bind_layers`` dissection rules
+(src/roce.py:324-348), plus the minimal ``IP``/``UDP``/``Raw`` layers the
+emit paths stack under them (src/roce_sq.py:1189-1193, src/roce_rq.py:719-723).
+
+Composition and building follow scapy's semantics: ``IP(dst=..)/UDP(..)/
+BTH(..)/RETH(..)/Raw(load=..)``; ``bytes(pkt)`` builds the innermost layer
+first and runs each layer's ``post_build`` on the way out, so
+``BTH.post_build`` -- exactly like src/roce.py:228-233 -- replaces the 4-byte
+ICRC trailer with ``compute_icrc`` when ``icrc is None``.
+
+The difference is where the CRC comes from: ``BTH.compute_icrc`` hands the
+wire frame to the HIP engine (``libroceicrc.so``, ``ricrc_compute_one``), and
+``emit_batch`` builds many frames and computes all their ICRCs in one GPU call
+(the batched emit path).  A non-IPv4/UDP
+underlayer gives a warning and ICRC 0, like the reference (src/roce.py:195-200,
+220-223).  There is no CPU fallback: without the engine, computing raises.
+"""
+
+from __future__ import annotations
+
+import copy
+import ipaddress
+import struct
+import warnings
+from typing import Optional
+
+import numpy as np
+
+ROCE_PORT = 4791  # src/roce_enum.py:14
+
+_transports = {"RC": 0x00, "UC": 0x20, "RD": 0x40, "UD": 0x60, "CNP": 0x80, "XRC": 0xA0}
+_ops = {
+    "SEND_FIRST": 0x00, "SEND_MIDDLE": 0x01, "SEND_LAST": 0x02, "SEND_LAST_WITH_IMMEDIATE": 0x03,
+    "SEND_ONLY": 0x04, "SEND_ONLY_WITH_IMMEDIATE": 0x05, "RDMA_WRITE_FIRST": 0x06,
+    "RDMA_WRITE_MIDDLE": 0x07, "RDMA_WRITE_LAST": 0x08, "RDMA_WRITE_LAST_WITH_IMMEDIATE": 0x09,
+    "RDMA_WRITE_ONLY": 0x0A, "RDMA_WRITE_ONLY_WITH_IMMEDIATE": 0x0B, "RDMA_READ_REQUEST": 0x0C,
+    "RDMA_READ_RESPONSE_FIRST": 0x0D, "RDMA_READ_RESPONSE_MIDDLE": 0x0E,
+    "RDMA_READ_RESPONSE_LAST": 0x0F, "RDMA_READ_RESPONSE_ONLY": 0x10, "ACKNOWLEDGE": 0x11,
+    "ATOMIC_ACKNOWLEDGE": 0x12, "COMPARE_SWAP": 0x13, "FETCH_ADD": 0x14, "RESYNC": 0x15,
+    "SEND_LAST_WITH_INVALIDATE": 0x16, "SEND_ONLY_WITH_INVALIDATE": 0x17,
+}
+CNP_OPCODE = 0x81
+
+
+def opcode(transport: str, op: str):
+    """src/roce.py:74-76."""
+    return (_transports[transport] + _ops[op], "{}_{}".format(transport, op))
+
+
+# Opcodes the reference lists per transport (src/roce.py:79-165).
+_per_transport = {
+    "RC": [o for o in _ops if o != "RESYNC"],
+    "UC": ["SEND_FIRST", "SEND_MIDDLE", "SEND_LAST", "SEND_LAST_WITH_IMMEDIATE", "SEND_ONLY",
+           "SEND_ONLY_WITH_IMMEDIATE", "RDMA_WRITE_FIRST", "RDMA_WRITE_MIDDLE", "RDMA_WRITE_LAST",
+           "RDMA_WRITE_LAST_WITH_IMMEDIATE", "RDMA_WRITE_ONLY", "RDMA_WRITE_ONLY_WITH_IMMEDIATE"],
+    "RD": [o for o in _ops if o not in ("SEND_LAST_WITH_INVALIDATE", "SEND_ONLY_WITH_INVALIDATE")],
+    "UD": ["SEND_ONLY", "SEND_ONLY_WITH_IMMEDIATE"],
+    "XRC": [o for o in _ops if o != "RESYNC"],
+}
+_bth_opcodes = dict(opcode(t, o) for t, ops in _per_transport.items() for o in ops)
+_bth_opcodes[CNP_OPCODE] = "CNP"
+
+
+# --------------------------------------------------------------------------
+# Minimal layer machinery (big-endian bit fields, '/' stacking, post_build)
+# --------------------------------------------------------------------------
+
+
+class Packet:
+    name = "Packet"
+    fields_desc: list = []  # (name, bits, default)
+
+    def __init__(self, _pkt: Optional[bytes] = None, **kw):
+        self.fields = {f[0]: f[2] for f in self.fields_desc}
+        self.payload: Optional[Packet] = None
+        self.underlayer: Optional[Packet] = None
+        for k, v in kw.items():
+            if k not in self.fields:
+                raise AttributeError(f"{self.name} has no field {k!r}")
+            self.fields[k] = v
+        if _pkt is not None:
+            self.dissect(bytes(_pkt))
+
+    # -- field access --------------------------------------------------------
+    def __getattr__(self, k):
+        fields = self.__dict__.get("fields")
+        if fields is not None and k in fields:
+            return fields[k]
+        raise AttributeError(k)
+
+    def __setattr__(self, k, v):
+        if "fields" in self.__dict__ and k in self.__dict__["fields"]:
+            self.__dict__["fields"][k] = v
+        else:
+            object.__setattr__(self, k, v)
+
+    # -- stacking ------------------------------------------------------------
+    def __truediv__(self, other):
+        if isinstance(other, (bytes, bytearray)):
+            other = Raw(load=bytes(other))
+        top = self.copy()
+        last = top
+        while last.payload is not None:
+            last = last.payload
+        o = other.copy()
+        last.payload = o
+        o.underlayer = last
+        return top
+
+    def copy(self):
+        c = copy.copy(self)
+        c.__dict__["fields"] = dict(self.fields)
+        if self.payload is not None:
+            p = self.payload.copy()
+            c.__dict__["payload"] = p
+            p.underlayer = c
+        return c
+
+    def layers(self):
+        layer = self
+        while layer is not None:
+            yield layer
+            layer = layer.payload
+
+    def getlayer(self, cls):
+        for layer in self.layers():
+            if isinstance(layer, cls):
+                return layer
+        return None
+
+    def __getitem__(self, cls):
+        layer = self.getlayer(cls)
+        if layer is None:
+            raise IndexError(f"Layer [{cls.__name__}] not found")
+        return layer
+
+    def __contains__(self, cls):
+        return self.getlayer(cls) is not None
+
+    # -- build ---------------------------------------------------------------
+    def self_build(self) -> bytes:
+        nbits = sum(f[1] for f in self.fields_desc)
+        v = 0
+        for name, bits, _ in self.fields_desc:
+            val = self.fields[name]
+            val = 0 if val is None else int(val)
+            v = (v << bits) | (val & ((1 << bits) - 1))
+        return v.to_bytes(nbits // 8, "big") if nbits else b""
+
+    def build_payload(self) -> bytes:
+        return self.payload.build() if self.payload is not None else b""
+
+    def post_build(self, p: bytes, pay: bytes) -> bytes:
+        return p + pay
+
+    def build(self) -> bytes:
+        return self.post_build(self.self_build(), self.build_payload())
+
+    def __bytes__(self):
+        return self.build()
+
+    def __len__(self):
+        return len(self.build())
+
+    # -- dissect -------------------------------------------------------------
+    def header_len(self) -> int:
+        return sum(f[1] for f in self.fields_desc) // 8
+
+    def dissect_fields(self, s: bytes) -> bytes:
+        hl = self.header_len()
+        if len(s) < hl:
+            raise ValueError(f"{self.name}: truncated ({len(s)} < {hl})")
+        v = int.from_bytes(s[:hl], "big")
+        shift = hl * 8
+        for name, bits, _ in self.fields_desc:
+            shift -= bits
+            self.fields[name] = (v >> shift) & ((1 << bits) - 1)
+        return s[hl:]
+
+    def next_layer(self, rest: bytes):
+        return Raw
+
+    def dissect(self, s: bytes) -> None:
+        rest = self.dissect_fields(s)
+        if rest:
+            cls = self.next_layer(rest)
+            if cls is not None:
+                pl = cls(rest)
+                self.payload = pl
+                pl.underlayer = self
+
+    def __repr__(self):
+        f = " ".join(f"{k}={v!r}" for k, v in self.fields.items())
+        inner = f" |{self.payload!r}" if self.payload is not None else ""
+        return f"<{self.name} {f}{inner}>"
+
+
+class Raw(Packet):
+    name = "Raw"
+    fields_desc = []
+
+    def __init__(self, _pkt=None, load: bytes = b""):
+        super().__init__()
+        self.__dict__["load"] = bytes(load)
+        if _pkt is not None:
+            self.__dict__["load"] = bytes(_pkt)
+
+    def self_build(self):
+        return self.load
+
+    def dissect(self, s):
+        self.__dict__["load"] = bytes(s)
+
+    def __repr__(self):
+        return f"<Raw load={self.load[:16]!r}{'...' if len(self.load) > 16 else ''}>"
+
+
+def _inet_checksum(data: bytes) -> int:
+    if len(data) % 2:
+        data += b"\0"
+    s = int(np.frombuffer(data, dtype=">u2").astype(np.uint64).sum())
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s) & 0xFFFF
+
+
+class IP(Packet):
+    """IPv4 with scapy's defaults (ihl/len/proto/chksum computed when None)."""
+
+    name = "IP"
+    fields_desc = [
+        ("version", 4, 4), ("ihl", 4, None), ("tos", 8, 0), ("len", 16, None), ("id", 16, 1),
+        ("flags", 3, 0), ("frag", 13, 0), ("ttl", 8, 64), ("proto", 8, None),
+        ("chksum", 16, None), ("src", 32, "127.0.0.1"), ("dst", 32, "127.0.0.1"),
+    ]
+
+    def _header(self, total_len: int, chksum: Optional[int]) -> bytes:
+        f = dict(self.fields)
+        f["ihl"] = 5 if f["ihl"] is None else f["ihl"]
+        f["len"] = total_len if f["len"] is None else f["len"]
+        if f["proto"] is None:
+            f["proto"] = 17 if isinstance(self.payload, UDP) else 0
+        f["src"] = int(ipaddress.IPv4Address(f["src"]))
+        f["dst"] = int(ipaddress.IPv4Address(f["dst"]))
+        f["chksum"] = 0 if chksum is None else chksum
+        v = 0
+        for name, bits, _ in self.fields_desc:
+            v = (v << bits) | (int(f[name]) & ((1 << bits) - 1))
+        return v.to_bytes(20, "big")
+
+    def self_build(self):
+        return b""  # built in post_build (needs the payload length)
+
+    def post_build(self, p, pay):
+        hdr = self._header(20 + len(pay), self.chksum)
+        if self.chksum is None:
+            hdr = hdr[:10] + struct.pack("!H", _inet_checksum(hdr)) + hdr[12:]
+        return hdr + pay
+
+    def header_len(self):
+        return 20
+
+    def dissect_fields(self, s):
+        rest = super().dissect_fields(s)
+        self.fields["src"] = str(ipaddress.IPv4Address(self.fields["src"]))
+        self.fields["dst"] = str(ipaddress.IPv4Address(self.fields["dst"]))
+        ihl = self.fields["ihl"]
+        return s[4 * ihl:]
+
+    def next_layer(self, rest):
+        return UDP if self.fields["proto"] == 17 else Raw
+
+
+class UDP(Packet):
+    name = "UDP"
+    fields_desc = [("sport", 16, 53), ("dport", 16, 53), ("len", 16, None), ("chksum", 16, None)]
+
+    def self_build(self):
+        return b""
+
+    def post_build(self, p, pay):
+        ln = 8 + len(pay) if self.len is None else self.len
+        hdr = struct.pack("!HHHH", self.sport, self.dport, ln, self.chksum or 0)
+        if self.chksum is None and isinstance(self.underlayer, IP):
+            ip = self.underlayer
+            pseudo = (ipaddress.IPv4Address(ip.src).packed + ipaddress.IPv4Address(ip.dst).packed
+                      + struct.pack("!BBH", 0, 17, ln))
+            c = _inet_checksum(pseudo + hdr + pay)
+            hdr = hdr[:6] + struct.pack("!H", c if c else 0xFFFF)
+        return hdr + pay
+
+    def header_len(self):
+        return 8
+
+    def next_layer(self, rest):
+        if ROCE_PORT in (self.fields["dport"], self.fields["sport"]):  # src/roce.py:347-348
+            return BTH
+        return Raw
+
+
+# --------------------------------------------------------------------------
+# RoCEv2 layers (src/roce.py)
+# --------------------------------------------------------------------------
+
+
+class BTH(Packet):
+    """Base Transport Header + ICRC trailer (src/roce.py:168-233)."""
+
+    name = "BTH"
+    fields_desc = [
+        ("opcode", 8, 0), ("solicited", 1, 0), ("migreq", 1, 0), ("padcount", 2, 0),
+        ("version", 4, 0), ("pkey", 16, 0xFFFF), ("fecn", 1, 0), ("becn", 1, 0), ("resv6", 6, 0),
+        ("dqpn", 24, 0), ("ackreq", 1, 0), ("resv7", 7, 0), ("psn", 24, 0),
+    ]
+
+    def __init__(self, _pkt=None, icrc: Optional[int] = None, **kw):
+        self.__dict__["icrc"] = icrc
+        super().__init__(_pkt, **kw)
+
+    def copy(self):
+        c = super().copy()
+        c.__dict__["icrc"] = self.icrc
+        return c
+
+    @staticmethod
+    def pack_icrc(icrc: int) -> bytes:
+        """src/roce.py:187-190: the wire bytes are the CRC little-endian."""
+        return struct.pack("!I", icrc & 0xFFFFFFFF)[::-1]
+
+    def compute_icrc(self, p: bytes) -> bytes:
+        """src/roce.py:192-223.  ``p`` is this layer's built bytes (BTH ..
+        trailer placeholder); the IPv4/UDP underlayers are rebuilt with their
+        final lengths and the whole wire frame goes to the HIP engine, which
+        applies the reference's masks and FF x 8 prefix itself."""
+        udp = self.underlayer
+        if udp is None or not isinstance(udp, UDP):
+            warnings.warn("Expecting UDP underlayer to compute checksum. Got %s."
+                          % (udp and udp.name))
+            return self.pack_icrc(0)
+        ip = udp.underlayer
+        if not isinstance(ip, IP):
+            warnings.warn("The underlayer protocol %s is not supported." % (ip and ip.name))
+            return self.pack_icrc(0)
+        frame = wire_frame(ip, udp, p)
+        icrc, status = get_engine().compute_one(frame)
+        return self.pack_icrc(icrc)
+
+    def build_payload(self):
+        trailer = struct.pack("!I", (self.icrc or 0) & 0xFFFFFFFF)  # FCSField "!I"
+        return super().build_payload() + trailer
+
+    def post_build(self, p, pay):
+        p += pay
+        if self.icrc is None:
+            p = p[:-4] + self.compute_icrc(p)
+        return p
+
+    def dissect(self, s):
+        # FCSField trailer: the last 4 bytes are BTH.icrc (src/roce.py:184)
+        body, trailer = s[:-4], s[-4:]
+        if len(trailer) == 4:
+            self.__dict__["icrc"] = struct.unpack("!I", trailer)[0]
+        rest = self.dissect_fields(body)
+        if rest:
+            cls = self.next_layer(rest)
+            pl = cls(rest)
+            self.payload = pl
+            pl.underlayer = self
+
+    def next_layer(self, rest):
+        return _BTH_BINDINGS.get(self.fields["opcode"], Raw)
+
+
+class _Ext(Packet):
+    def next_layer(self, rest):
+        return Raw
+
+
+class AETH(_Ext):
+    name = "AETH"
+    fields_desc = [("rsvd", 1, 0), ("code", 2, 2), ("value", 5, 0), ("msn", 24, 0)]
+    _codes = {"ACK": 0, "RNR": 1, "RSVD": 2, "NAK": 3}
+
+    def __init__(self, _pkt=None, **kw):
+        if isinstance(kw.get("code"), str):
+            kw["code"] = self._codes[kw["code"]]
+        super().__init__(_pkt, **kw)
+
+
+class RETH(_Ext):
+    name = "RETH"
+    fields_desc = [("va", 64, 0), ("rkey", 32, 0), ("dlen", 32, 0)]
+
+
+class AtomicETH(_Ext):
+    name = "AtomicETH"
+    fields_desc = [("va", 64, 0), ("rkey", 32, 0), ("swap", 64, 0), ("comp", 64, 0)]
+
+
+class AtomicAckETH(_Ext):
+    name = "AtomicAckETH"
+    fields_desc = [("orig", 64, 0)]
+
+
+class ImmDt(_Ext):
+    name = "ImmDt"
+    fields_desc = [("data", 32, 0)]
+
+
+class IETH(_Ext):
+    name = "IETH"
+    fields_desc = [("rkey", 32, 0)]
+
+
+class RETHImmDt(_Ext):
+    name = "RETHImmdt"
+    fields_desc = [("va", 64, 0), ("rkey", 32, 0), ("dlen", 32, 0), ("data", 32, 0)]
+
+
+class CNPPadding(_Ext):
+    name = "CNPPadding"
+    fields_desc = [("reserved1", 64, 0), ("reserved2", 64, 0)]
+
+
+class GRH(Packet):
+    name = "GRH"
+    fields_desc = [
+        ("ipver", 4, 6), ("tclass", 8, 0), ("flowlabel", 20, 6), ("paylen", 16, 0),
+        ("nexthdr", 8, 0), ("hoplmt", 8, 0), ("sgid", 128, 0), ("dgid", 128, 0),
+    ]
+
+    def next_layer(self, rest):
+        return BTH
+
+
+def cnp(dqpn: int) -> BTH:
+    """src/roce.py:244-246."""
+    return BTH(opcode=CNP_OPCODE, becn=1, dqpn=dqpn) / CNPPadding()
+
+
+# bind_layers (src/roce.py:324-348): which header follows BTH for an opcode
+_BTH_BINDINGS = {
+    CNP_OPCODE: CNPPadding,
+    opcode("RC", "ACKNOWLEDGE")[0]: AETH,
+    opcode("RC", "ATOMIC_ACKNOWLEDGE")[0]: AETH,
+    opcode("RC", "RDMA_READ_RESPONSE_FIRST")[0]: AETH,
+    opcode("RC", "RDMA_READ_RESPONSE_LAST")[0]: AETH,
+    opcode("RC", "RDMA_READ_RESPONSE_ONLY")[0]: AETH,
+    opcode("RC", "COMPARE_SWAP")[0]: AtomicETH,
+    opcode("RC", "FETCH_ADD")[0]: AtomicETH,
+    opcode("RC", "SEND_LAST_WITH_INVALIDATE")[0]: IETH,
+    opcode("RC", "SEND_ONLY_WITH_INVALIDATE")[0]: IETH,
+    opcode("RC", "SEND_LAST_WITH_IMMEDIATE")[0]: ImmDt,
+    opcode("RC", "SEND_ONLY_WITH_IMMEDIATE")[0]: ImmDt,
+    opcode("RC", "RDMA_WRITE_LAST_WITH_IMMEDIATE")[0]: ImmDt,
+    opcode("RC", "RDMA_READ_REQUEST")[0]: RETH,
+    opcode("RC", "RDMA_WRITE_FIRST")[0]: RETH,
+    opcode("RC", "RDMA_WRITE_ONLY")[0]: RETH,
+    opcode("RC", "RDMA_WRITE_ONLY_WITH_IMMEDIATE")[0]: RETHImmDt,
+}
+
+
+# --------------------------------------------------------------------------
+# Engine plumbing, emit and receive helpers
+# --------------------------------------------------------------------------
+
+_engine = None
+
+
+def get_engine():
+    """The process-wide HIP engine (device from ROCE_ICRC_DEVICE, default 0).
+    Raises IcrcUnavailable when the library or a gfx950 GPU is missing."""
+    global _engine
+    if _engine is None:
+        import os
+
+        from .engine import IcrcEngine
+        _engine = IcrcEngine(int(os.environ.get("ROCE_ICRC_DEVICE", "0")))
+    return _engine
+
+
+def set_engine(engine) -> None:
+    """Use an existing IcrcEngine (e.g. one per gRPC worker thread)."""
+    global _engine
+    _engine = engine
+
+
+def wire_frame(ip: IP, udp: UDP, roce: bytes) -> bytes:
+    """IPv4 + UDP headers (lengths final, checksums as the fields say or 0 --
+    both are ICRC-masked) in front of the built BTH bytes ``roce``."""
+    ulen = 8 + len(roce) if udp.len is None else udp.len
+    udp_hdr = struct.pack("!HHHH", udp.sport, udp.dport, ulen, udp.chksum or 0)
+    ip_hdr = ip._header(20 + 8 + len(roce), ip.chksum)
+    return ip_hdr + udp_hdr + roce
+
+
+def add_padding_if_needed(pkt: Packet) -> Packet:
+    """src/roce_util.py:187-199: zero-pad the Raw load to a multiple of 4 and
+    set BTH.padcount."""
+    if Raw in pkt:
+        raw = pkt[Raw]
+        padcount = len(raw.load) % 4
+        if padcount:
+            raw.__dict__["load"] = raw.load + b"\0" * (4 - padcount)
+            pkt[BTH].padcount = 4 - padcount
+    return pkt
+
+
+def l3_packet(pkt: Packet, dst: str, sport: int, src: str = "127.0.0.1") -> Packet:
+    """The emit-side wrap of src/roce_sq.py:1186-1193 / src/roce_rq.py:718-723:
+    pad, then IP(dst)/UDP(dport=4791, sport=<own QPN>)/pkt."""
+    if Raw in pkt:
+        pkt = add_padding_if_needed(pkt.copy())
+    return IP(src=src, dst=dst) / UDP(dport=ROCE_PORT, sport=sport) / pkt
+
+
+def emit_batch(pkts: list[Packet]) -> list[bytes]:
+    """Build many IPv4 RoCE packets with ONE GPU ICRC call (the batched form of
+    calling ``bytes(pkt)`` per packet, which is what scapy's send() does at
+    src/roce_sq.py:1197 and src/roce_rq.py:731).  BTH layers with an explicit
+    ``icrc`` keep it; the UDP checksum is recomputed over the final trailer."""
+    frames, need = [], []
+    for i, pkt in enumerate(pkts):
+        bth = pkt.getlayer(BTH)
+        if bth is None or bth.icrc is not None:
+            frames.append(pkt.build())
+            continue
+        placeholder = pkt.copy()
+        placeholder[BTH].__dict__["icrc"] = 0
+        frames.append(placeholder.build())
+        need.append(i)
+    if need:
+        offs = np.zeros(len(need), np.uint64)
+        lens = np.zeros(len(need), np.uint32)
+        parts, pos = [], 0
+        for j, i in enumerate(need):
+            offs[j] = pos
+            lens[j] = len(frames[i])
+            parts.append(frames[i])
+            pos += len(frames[i])
+        icrc, _ = get_engine().compute_batch(np.frombuffer(b"".join(parts), np.uint8), offs, lens)
+        for j, i in enumerate(need):
+            f = bytearray(frames[i])
+            f[-4:] = BTH.pack_icrc(int(icrc[j]))
+            ip = pkts[i].getlayer(IP)
+            udp = pkts[i].getlayer(UDP)
+            ihl = 4 * (f[0] & 0xF)
+            if udp is not None and udp.chksum is None and ip is not None:
+                f[ihl + 6:ihl + 8] = b"\0\0"
+                pseudo = bytes(f[12:20]) + struct.pack("!BBH", 0, 17, len(f) - ihl)
+                c = _inet_checksum(pseudo + bytes(f[ihl:]))
+                f[ihl + 6:ihl + 8] = struct.pack("!H", c if c else 0xFFFF)
+            frames[i] = bytes(f)
+    return frames
+
+
+def verify_frames(frames: list[bytes]) -> np.ndarray:
+    """Receive-side ICRC check over full IPv4 frames (new behaviour: the
+    reference never verifies), one GPU call."""
+    offs = np.zeros(len(frames), np.uint64)
+    lens = np.array([len(f) for f in frames], np.uint32)
+    if len(frames) > 1:
+        offs[1:] = np.cumsum(lens[:-1])
+    ok, _, _ = get_engine().verify_batch(np.frombuffer(b"".join(frames), np.uint8), offs, lens)
+    return ok
