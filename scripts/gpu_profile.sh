@@ -17,7 +17,7 @@ timeout -k 10 600 python bench.py --workload $WL > $OUT/bench_$TAG.json 2> $OUT/
 rc=$?; cat $OUT/bench_$TAG.json; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$TAG.err; exit $rc; }
 cd /tmp && export TMPDIR=/tmp
 echo "== rocprofv3 kernel trace"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > $OUT/prof_$TAG.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $R/bench.py --workload $WL --no-cpu-baseline --no-e2e > $OUT/prof_$TAG.log 2>&1
 rc=$?; tail -3 $OUT/prof_$TAG.log; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 echo "== pmc FETCH_SIZE"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmcf_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmcf_$TAG.log 2>&1
@@ -25,5 +25,11 @@ rc=$?; tail -2 $OUT/pmcf_$TAG.log; echo "pmcf rc=$rc"; [ $rc -eq 0 ] || exit $rc
 echo "== pmc WRITE_SIZE"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcw_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmcw_$TAG.log 2>&1
 rc=$?; tail -2 $OUT/pmcw_$TAG.log; echo "pmcw rc=$rc"; [ $rc -eq 0 ] || exit $rc
-find $OUT/prof_$TAG $OUT/pmcf_$TAG -name "*.csv" | head
+cd $R
+python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
+  --packets $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][1])") \
+  --frame-bytes $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][0] + 44)") \
+  --out $OUT/pmc_traffic_$TAG.json || exit 1
+python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json > $OUT/prof_summary_$TAG.txt || exit 1
+cat $OUT/prof_summary_$TAG.txt
 exit 0
