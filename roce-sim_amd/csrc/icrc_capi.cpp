@@ -67,16 +67,18 @@ int auto_log2g(uint32_t len) {
   return l;
 }
 
-// Device-resident ragged batches: lengths live on the device, so the lane
-// count comes from the context setting or this typical length (the mean frame
-// of the BASELINE mixed-MTU configuration, 1632 B).
+// Ragged batches are counting-sorted by iteration count inside each
+// workgroup's window, so their sets are size-homogeneous and longer lane runs
+// pay off: one notch more lanes than a uniform batch of the same mean length
+// (mixed-MTU mean 1.6 KiB -> G = 8, measured best).  Device-resident ragged
+// calls do not know the lengths on the host: they use the mixed-MTU choice.
 constexpr uint32_t kRaggedTypicalLen = 1632;
-
-int pick_log2g(const ricrc_ctx* c, uint32_t typical_len) {
-  return c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(typical_len);
+int ragged_log2g(const ricrc_ctx* c, uint32_t mean) {
+  if (c->lanes > 0) return log2_lanes(c->lanes);
+  const int l = auto_log2g(mean) + 1;
+  return l > 4 ? 4 : l;
 }
 
-// Device-resident calls run on the caller's stream; NULL is the HIP null stream.
 hipStream_t pick_stream(const ricrc_ctx*, void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 int ensure_frames(ricrc_ctx* c, size_t bytes) {
@@ -160,7 +162,7 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
   HIP_TRY(
       hipMemcpyAsync(c->d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
   rc = launch(c, c->d_frames, c->d_offs, c->d_lens, 0, 0, n, c->d_icrc, c->d_status,
-              verify ? c->d_ok : nullptr, true, verify, pick_log2g(c, mean_len(lens, n)),
+              verify ? c->d_ok : nullptr, true, verify, ragged_log2g(c, mean_len(lens, n)),
               c->stream);
   if (rc) return rc;
   if (icrc_out)
@@ -385,7 +387,7 @@ int ricrc_compute_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_
   // lanes per packet for ragged device batches: the context setting, else the
   // 1 KiB-MTU choice (lengths are on the device; no host round trip)
   return launch(c, d_frames, d_offsets, d_lens, 0, 0, n, d_icrc, d_status, nullptr, true, false,
-                pick_log2g(c, kRaggedTypicalLen), pick_stream(c, stream));
+                ragged_log2g(c, kRaggedTypicalLen), pick_stream(c, stream));
 }
 
 int ricrc_verify_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_t* d_offsets,
@@ -393,7 +395,7 @@ int ricrc_verify_batch_dev(ricrc_ctx* c, const uint8_t* d_frames, const uint64_t
                            uint8_t* d_status, void* stream) {
   if (!c || !d_ok || (n && (!d_frames || !d_offsets || !d_lens))) return RICRC_EINVAL;
   return launch(c, d_frames, d_offsets, d_lens, 0, 0, n, d_icrc, d_status, d_ok, true, true,
-                pick_log2g(c, kRaggedTypicalLen), pick_stream(c, stream));
+                ragged_log2g(c, kRaggedTypicalLen), pick_stream(c, stream));
 }
 
 int ricrc_compute_strided_dev(ricrc_ctx* c, const uint8_t* d_frames, uint64_t stride, uint32_t len,

@@ -273,34 +273,132 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, u
                         gl, base);
 }
 
-template <int LOG2G, bool RAGGED, bool VERIFY>
-__global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
+// LDS staging of the folding tables (every kernel, once per workgroup).
+template <int LOG2G>
+__device__ __forceinline__ void stage_tables(const IcrcArgs& a, int tid) {
+  constexpr int NCOMB = 1 + LOG2G;
+  const uint32_t* gm = a.tables + LOG2G * 1024;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = tid + r * 1024;  // 8192 16-byte quads
+    const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
+    lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16),
+            gm[tab * 256 + e]);
+  }
+  const uint32_t* gc = a.tables + kNumMainSets * 1024;
+  for (int i = tid; i < NCOMB * 1024; i += 1024) lds_wr(kLdsMain + 4u * i, gc[i]);
+}
+
+// One packet by its group of G lanes: load, fold, combine, check, emit.
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void process_packet(const IcrcArgs& a, uint32_t pkt, bool live,
+                                               uint64_t off, uint32_t L, int gl, int base,
+                                               uint32_t kc0, uint32_t kc1) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
+  constexpr int U = kUnroll;
+  const Pkt p = describe<DPI>(a.frames, pkt, live, off, L);
+
+  // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
+  // U (the first block holds the remainder), then the last one (J-1), which
+  // skips columns past the end and may also need the fix-ups.  The head
+  // chunks, the first body block and the last chunk are issued together.
+  const int JL = p.J - 1;
+  const int jhh = min(p.jh, JL);
+  const int nbody = JL - jhh;
+  const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
+  const int nblk = (nbody + U - 1) / U;
+  uint32_t trailer = 0;
+  if (VERIFY && !p.dead && gl == 0) trailer = ldg32(p.fp + p.L - 4);
+  const u32x4 wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
+  const u32x4 wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
+  u32x4 cur[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
+  const u32x4 wl = load_chunk<G>(p, JL, gl);
+
+  Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  uint32_t h0 = 0, h2 = 0;
+  for (int j = 0; j < jhh; ++j) {
+    u32x4 w = (j == 0) ? wh0 : (j == 1) ? wh1 : load_chunk<G>(p, j, gl);
+    fix_chunk(w, DPI * j + 4 * gl - p.S, 6, 8, h0, h2);
+    fold(A, w, kc0, kc1);
+  }
+  // body blocks, ping-pong between cur and nxt (no register copies)
+  int j0 = jhh, bs = first;
+  u32x4 nxt[U];
+  for (int b = 0; b < nblk; b += 2) {
+    int jn = j0 + bs;
+    if (b + 1 < nblk) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < bs) fold(A, cur[u], kc0, kc1);
+    if (b + 1 >= nblk) break;
+    j0 = jn;
+    jn = j0 + U;
+    if (b + 2 < nblk) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = load_body<G>(p, jn + u, gl);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) fold(A, nxt[u], kc0, kc1);
+    j0 = jn;
+    bs = U;
+  }
+  {
+    u32x4 w = wl;
+    const int kb = DPI * JL + 4 * gl - p.S;
+    if (JL < p.jh) fix_chunk(w, kb, 6, 8, h0, h2);
+    fold_last(A, w, kb, p.n, kc0, kc1);
+  }
+
+  // ---- packet done: fold the group, check the header, emit ----------------
+  uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                              A.P[3] ^ A.T[3], p.r, gl, base);
+  const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
+  const uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
+  uint32_t st = p.dead ? kPktBadLen : 0u;
+  const int ihl = (int)(d0 & 0xFu);
+  if (st == 0) {
+    if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
+      st |= kPktNotIpv4;
+    else if (((d2 >> 8) & 0xFFu) != 17u)
+      st |= kPktNotUdp;
+    else if (p.L < (uint32_t)(4 * ihl + 24))
+      st |= kPktBadLen;
+    const uint32_t tot = ((d0 >> 8) & 0xFF00u) | (d0 >> 24);
+    if (tot != p.L) st |= kPktLenMismatch;
+  }
+  const bool good = (st & kPktFatal) == 0;
+  if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kc0, kc1);
+  const uint32_t icrc = good ? ~B : 0u;
+  if (live && gl == 0) {
+    if constexpr (VERIFY) {
+      const bool ok = good && trailer == icrc;
+      if (good && !ok) st |= kPktIcrcMismatch;
+      a.ok_out[pkt] = ok ? 1 : 0;
+    }
+    if (a.icrc_out) a.icrc_out[pkt] = icrc;
+    if (a.status_out) a.status_out[pkt] = (uint8_t)st;
+  }
+}
+
+// Fixed-size frames at frames + i * stride.
+template <int LOG2G, bool VERIFY>
+__global__ void __launch_bounds__(1024, 1) icrc_strided_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;  // packets per wave step
-  constexpr int DPI = 4 * G;   // grid dwords per iteration
-  constexpr int NCOMB = 1 + LOG2G;
-  constexpr int U = kUnroll;
   const int tid = threadIdx.x;
-
-  // ---- stage the folding tables in LDS ------------------------------------
-  {
-    const uint32_t* gm = a.tables + LOG2G * 1024;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = tid + r * 1024;  // 8192 16-byte quads
-      const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
-      lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16),
-              gm[tab * 256 + e]);
-    }
-    const uint32_t* gc = a.tables + kNumMainSets * 1024;
-    for (int i = tid; i < NCOMB * 1024; i += 1024) lds_wr(kLdsMain + 4u * i, gc[i]);
-  }
+  stage_tables<LOG2G>(a, tid);
   __syncthreads();
 
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
   const int grp = lane >> LOG2G;
-  const int base = grp * G;
   const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
   const uint32_t kc1 = kc0 | 0x10000u;
   // Each workgroup owns a contiguous range of packet sets, so every CU sweeps
@@ -310,109 +408,104 @@ __global__ void __launch_bounds__(1024, 1) icrc_kernel(IcrcArgs a) {
   const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
   const uint32_t set_begin = blockIdx.x * per_block;
   const uint32_t set_end = min(nsets, set_begin + per_block);
-
   for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
     const uint32_t pkt = set * PPW + grp;
     const bool live = pkt < a.n;
-    uint64_t off = 0;
-    uint32_t L = 0;
-    if (live) {
-      if constexpr (RAGGED) {
-        off = a.offsets[pkt];
-        L = a.lens[pkt];
-      } else {
-        off = (uint64_t)pkt * a.stride;
-        L = a.len;
-      }
-    }
-    const Pkt p = describe<DPI>(a.frames, pkt, live, off, L);
+    process_packet<LOG2G, VERIFY>(a, pkt, live, live ? (uint64_t)pkt * a.stride : 0,
+                                  live ? a.len : 0, gl, grp * G, kc0, kc1);
+  }
+}
 
-    // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
-    // U (the first block holds the remainder), then the last one (J-1), which
-    // skips columns past the end and may also need the fix-ups.  The head
-    // chunks, the first body block and the last chunk are issued together.
-    const int JL = p.J - 1;
-    const int jhh = min(p.jh, JL);
-    const int nbody = JL - jhh;
-    const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
-    const int nblk = (nbody + U - 1) / U;
-    uint32_t trailer = 0;
-    if (VERIFY && !p.dead && gl == 0) trailer = ldg32(p.fp + p.L - 4);
-    const u32x4 wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
-    const u32x4 wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
-    u32x4 cur[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
-    const u32x4 wl = load_chunk<G>(p, JL, gl);
+// Ragged frames (offsets[i], lens[i]).  The lanes of a wave fold their
+// packets in lockstep, so a wave waits for the longest packet of its set.
+// Each workgroup therefore takes a contiguous window of packets (locality
+// kept) and counting-sorts it in LDS by iteration count; waves then take
+// size-homogeneous sets of the sorted window, round robin.
+template <int LOG2G>
+struct RaggedLds {
+  static constexpr int kNComb = 1 + LOG2G;
+  static constexpr uint32_t kBase = kLdsMain + 4096u * kNComb;
+  static constexpr int kBuckets = 128;
+  static constexpr uint32_t kHist = kBase;               // kBuckets x u32 counts / cursors
+  static constexpr uint32_t kPerm = kBase + 4 * kBuckets;  // window x u16 local indices
+  static constexpr int kAvail = (int)(163840u - kPerm);
+  static constexpr int kWindow = (kAvail / 2 >= 4096) ? 4096 : (kAvail / 2) / 64 * 64;
+  static constexpr uint32_t kBytes = kPerm + 2 * kWindow;
+};
 
-    Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    uint32_t h0 = 0, h2 = 0;
-    for (int j = 0; j < jhh; ++j) {
-      u32x4 w = (j == 0) ? wh0 : (j == 1) ? wh1 : load_chunk<G>(p, j, gl);
-      fix_chunk(w, DPI * j + 4 * gl - p.S, 6, 8, h0, h2);
-      fold(A, w, kc0, kc1);
-    }
-    // body blocks, ping-pong between cur and nxt (no register copies)
-    int j0 = jhh, bs = first;
-    u32x4 nxt[U];
-    for (int b = 0; b < nblk; b += 2) {
-      int jn = j0 + bs;
-      if (b + 1 < nblk) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (u < bs) fold(A, cur[u], kc0, kc1);
-      if (b + 1 >= nblk) break;
-      j0 = jn;
-      jn = j0 + U;
-      if (b + 2 < nblk) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = load_body<G>(p, jn + u, gl);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) fold(A, nxt[u], kc0, kc1);
-      j0 = jn;
-      bs = U;
-    }
-    {
-      u32x4 w = wl;
-      const int kb = DPI * JL + 4 * gl - p.S;
-      if (JL < p.jh) fix_chunk(w, kb, 6, 8, h0, h2);
-      fold_last(A, w, kb, p.n, kc0, kc1);
-    }
+template <int LOG2G, bool VERIFY>
+__global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int PPW = 64 / G;
+  constexpr int DPI = 4 * G;
+  using LD = RaggedLds<LOG2G>;
+  constexpr int W = LD::kWindow;
+  constexpr int NB = LD::kBuckets;
+  const int tid = threadIdx.x;
+  stage_tables<LOG2G>(a, tid);
 
-    // ---- packet done: fold the group, check the header, emit ----------------
-    uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
-                                A.P[3] ^ A.T[3], p.r, gl, base);
-    const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
-    const uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
-    uint32_t st = p.dead ? kPktBadLen : 0u;
-    const int ihl = (int)(d0 & 0xFu);
-    if (st == 0) {
-      if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
-        st |= kPktNotIpv4;
-      else if (((d2 >> 8) & 0xFFu) != 17u)
-        st |= kPktNotUdp;
-      else if (p.L < (uint32_t)(4 * ihl + 24))
-        st |= kPktBadLen;
-      const uint32_t tot = ((d0 >> 8) & 0xFF00u) | (d0 >> 24);
-      if (tot != p.L) st |= kPktLenMismatch;
-    }
-    const bool good = (st & kPktFatal) == 0;
-    if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kc0, kc1);
-    const uint32_t icrc = good ? ~B : 0u;
-    if (live && gl == 0) {
-      if constexpr (VERIFY) {
-        const bool ok = good && trailer == icrc;
-        if (good && !ok) st |= kPktIcrcMismatch;
-        a.ok_out[pkt] = ok ? 1 : 0;
+  const int lane = tid & 63;
+  const int gl = lane & (G - 1);
+  const int grp = lane >> LOG2G;
+  const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
+  const uint32_t kc1 = kc0 | 0x10000u;
+  const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
+  const uint32_t p0 = blockIdx.x * per_block;
+  const uint32_t p1 = min(a.n, p0 + per_block);
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  lds_u32* hist = (lds_u32*)(uintptr_t)LD::kHist;
+  lds_u16* perm = (lds_u16*)(uintptr_t)LD::kPerm;
+
+  for (uint32_t w0 = p0; w0 < p1; w0 += W) {
+    const int cnt = (int)min((uint32_t)W, p1 - w0);
+    if (tid < NB) hist[tid] = 0;
+    __syncthreads();
+    // iteration count of every packet of the window -> bucket
+    int keys[(W + 1023) / 1024];
+#pragma unroll
+    for (int r = 0; r < (W + 1023) / 1024; ++r) {
+      const int i = tid + r * 1024;
+      int key = 0;
+      if (i < cnt) {
+        const uint32_t L = a.lens[w0 + i];
+        const uint64_t off = a.offsets[w0 + i];
+        if (!(L < 44 || (L & 3u) || L > 65535u)) {
+          const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
+          key = min(NB - 1, (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
+        }
+        atomicAdd((uint32_t*)&hist[key], 1u);
       }
-      if (a.icrc_out) a.icrc_out[pkt] = icrc;
-      if (a.status_out) a.status_out[pkt] = (uint8_t)st;
+      keys[r] = key;
     }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of NB = 128 counts by one wave (2 per lane)
+      const uint32_t c0 = hist[2 * tid], c1 = hist[2 * tid + 1];
+      uint32_t s = c0 + c1;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)s, d, 64);
+        if (tid >= d) s += t;
+      }
+      const uint32_t excl = s - c0 - c1;
+      hist[2 * tid] = excl;
+      hist[2 * tid + 1] = excl + c0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < (W + 1023) / 1024; ++r) {
+      const int i = tid + r * 1024;
+      if (i < cnt) perm[atomicAdd((uint32_t*)&hist[keys[r]], 1u)] = (uint16_t)i;
+    }
+    __syncthreads();
+    const int nsets = (cnt + PPW - 1) / PPW;
+    for (int set = tid >> 6; set < nsets; set += 16) {
+      const int idx = set * PPW + grp;
+      const bool live = idx < cnt;
+      const uint32_t pkt = live ? w0 + perm[idx] : 0;
+      process_packet<LOG2G, VERIFY>(a, pkt, live, live ? a.offsets[pkt] : 0,
+                                    live ? a.lens[pkt] : 0, gl, grp * G, kc0, kc1);
+    }
+    __syncthreads();
   }
 }
 
@@ -442,9 +535,8 @@ typedef void (*kernel_fn)(IcrcArgs);
 
 template <int LOG2G>
 kernel_fn pick(bool ragged, bool verify) {
-  if (ragged)
-    return verify ? icrc_kernel<LOG2G, true, true> : icrc_kernel<LOG2G, true, false>;
-  return verify ? icrc_kernel<LOG2G, false, true> : icrc_kernel<LOG2G, false, false>;
+  if (ragged) return verify ? icrc_ragged_kernel<LOG2G, true> : icrc_ragged_kernel<LOG2G, false>;
+  return verify ? icrc_strided_kernel<LOG2G, true> : icrc_strided_kernel<LOG2G, false>;
 }
 
 kernel_fn select_kernel(int log2g, bool ragged, bool verify) {
@@ -460,7 +552,18 @@ kernel_fn select_kernel(int log2g, bool ragged, bool verify) {
   }
 }
 
-size_t lds_bytes(int log2g) { return kLdsMain + 4096u * (1 + log2g); }
+size_t lds_bytes(int log2g, bool ragged) {
+  if (!ragged) return kLdsMain + 4096u * (1 + log2g);
+  switch (log2g) {
+    case 0: return RaggedLds<0>::kBytes;
+    case 1: return RaggedLds<1>::kBytes;
+    case 2: return RaggedLds<2>::kBytes;
+    case 3: return RaggedLds<3>::kBytes;
+    case 4: return RaggedLds<4>::kBytes;
+    case 5: return RaggedLds<5>::kBytes;
+    default: return RaggedLds<6>::kBytes;
+  }
+}
 
 }  // namespace
 
@@ -477,7 +580,7 @@ hipError_t prepare_kernels() {
       for (int v = 0; v < 2; ++v) {
         hipError_t e = hipFuncSetAttribute((const void*)select_kernel(l, r, v),
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_bytes(l));
+                                           (int)lds_bytes(l, r));
         if (e != hipSuccess) return e;
       }
   return hipSuccess;
@@ -493,7 +596,7 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   uint64_t blocks = (nsets + 15) / 16;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), lds_bytes(log2g), stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), lds_bytes(log2g, ragged), stream, a);
   return hipGetLastError();
 }
 
