@@ -67,6 +67,10 @@ int auto_log2g(uint32_t len) {
   return l;
 }
 
+int pick_log2g(const ricrc_ctx* c, uint32_t typical_len) {
+  return c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(typical_len);
+}
+
 // Ragged batches are counting-sorted by iteration count inside each
 // workgroup's window, so their sets are size-homogeneous and longer lane runs
 // pay off: one notch more lanes than a uniform batch of the same mean length
