@@ -289,60 +289,77 @@ __device__ __forceinline__ void stage_tables(const IcrcArgs& a, int tid) {
   for (int i = tid; i < NCOMB * 1024; i += 1024) lds_wr(kLdsMain + 4u * i, gc[i]);
 }
 
-// One packet by its group of G lanes: load, fold, combine, check, emit.
+// A packet's first batch of loads: head chunks, the first body block and the
+// last chunk (plus the trailer in verify mode).  Issued one packet set ahead
+// so small packets do not wait a full HBM round trip per set.
+template <int U>
+struct Batch {
+  u32x4 wh0, wh1, wl;
+  u32x4 cur[U];
+  uint32_t trailer;
+};
+
 template <int LOG2G, bool VERIFY>
-__device__ __forceinline__ void process_packet(const IcrcArgs& a, uint32_t pkt, bool live,
-                                               uint64_t off, uint32_t L, int gl, int base,
-                                               uint32_t kc0, uint32_t kc1) {
+__device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int U = kUnroll;
+  Batch<U> b;
+  const int JL = p.J - 1;
+  const int jhh = min(p.jh, JL);
+  const int nbody = JL - jhh;
+  const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
+  b.trailer = 0;
+  if (VERIFY && !p.dead && gl == 0) b.trailer = ldg32(p.fp + p.L - 4);
+  b.wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
+  b.wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    b.cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
+  b.wl = load_chunk<G>(p, JL, gl);
+  return b;
+}
+
+// Fold, combine, check and emit one packet whose first batch is in `b`.
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, Batch<kUnroll>& b,
+                                              int gl, int base, uint32_t kc0, uint32_t kc1) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   constexpr int U = kUnroll;
-  const Pkt p = describe<DPI>(a.frames, pkt, live, off, L);
-
   // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
   // U (the first block holds the remainder), then the last one (J-1), which
-  // skips columns past the end and may also need the fix-ups.  The head
-  // chunks, the first body block and the last chunk are issued together.
+  // skips columns past the end and may also need the fix-ups.
   const int JL = p.J - 1;
   const int jhh = min(p.jh, JL);
   const int nbody = JL - jhh;
   const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
   const int nblk = (nbody + U - 1) / U;
-  uint32_t trailer = 0;
-  if (VERIFY && !p.dead && gl == 0) trailer = ldg32(p.fp + p.L - 4);
-  const u32x4 wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
-  const u32x4 wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
-  u32x4 cur[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
-  const u32x4 wl = load_chunk<G>(p, JL, gl);
 
   Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < jhh; ++j) {
-    u32x4 w = (j == 0) ? wh0 : (j == 1) ? wh1 : load_chunk<G>(p, j, gl);
+    u32x4 w = (j == 0) ? b.wh0 : (j == 1) ? b.wh1 : load_chunk<G>(p, j, gl);
     fix_chunk(w, DPI * j + 4 * gl - p.S, 6, 8, h0, h2);
     fold(A, w, kc0, kc1);
   }
-  // body blocks, ping-pong between cur and nxt (no register copies)
+  // body blocks, ping-pong between b.cur and nxt (no register copies)
   int j0 = jhh, bs = first;
   u32x4 nxt[U];
-  for (int b = 0; b < nblk; b += 2) {
+  for (int bk = 0; bk < nblk; bk += 2) {
     int jn = j0 + bs;
-    if (b + 1 < nblk) {
+    if (bk + 1 < nblk) {
 #pragma unroll
       for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (u < bs) fold(A, cur[u], kc0, kc1);
-    if (b + 1 >= nblk) break;
+      if (u < bs) fold(A, b.cur[u], kc0, kc1);
+    if (bk + 1 >= nblk) break;
     j0 = jn;
     jn = j0 + U;
-    if (b + 2 < nblk) {
+    if (bk + 2 < nblk) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = load_body<G>(p, jn + u, gl);
+      for (int u = 0; u < U; ++u) b.cur[u] = load_body<G>(p, jn + u, gl);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) fold(A, nxt[u], kc0, kc1);
@@ -350,13 +367,13 @@ __device__ __forceinline__ void process_packet(const IcrcArgs& a, uint32_t pkt, 
     bs = U;
   }
   {
-    u32x4 w = wl;
+    u32x4 w = b.wl;
     const int kb = DPI * JL + 4 * gl - p.S;
     if (JL < p.jh) fix_chunk(w, kb, 6, 8, h0, h2);
     fold_last(A, w, kb, p.n, kc0, kc1);
   }
 
-  // ---- packet done: fold the group, check the header, emit ----------------
+  // ---- packet done: fold the group, check the header, emit ------------------
   uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
                               A.P[3] ^ A.T[3], p.r, gl, base);
   const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
@@ -376,14 +393,14 @@ __device__ __forceinline__ void process_packet(const IcrcArgs& a, uint32_t pkt, 
   const bool good = (st & kPktFatal) == 0;
   if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kc0, kc1);
   const uint32_t icrc = good ? ~B : 0u;
-  if (live && gl == 0) {
+  if (p.live && gl == 0) {
     if constexpr (VERIFY) {
-      const bool ok = good && trailer == icrc;
+      const bool ok = good && b.trailer == icrc;
       if (good && !ok) st |= kPktIcrcMismatch;
-      a.ok_out[pkt] = ok ? 1 : 0;
+      a.ok_out[p.pkt] = ok ? 1 : 0;
     }
-    if (a.icrc_out) a.icrc_out[pkt] = icrc;
-    if (a.status_out) a.status_out[pkt] = (uint8_t)st;
+    if (a.icrc_out) a.icrc_out[p.pkt] = icrc;
+    if (a.status_out) a.status_out[p.pkt] = (uint8_t)st;
   }
 }
 
@@ -408,11 +425,19 @@ __global__ void __launch_bounds__(1024, 1) icrc_strided_kernel(IcrcArgs a) {
   const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
   const uint32_t set_begin = blockIdx.x * per_block;
   const uint32_t set_end = min(nsets, set_begin + per_block);
-  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
+  constexpr int DPI = 4 * G;
+  auto make = [&](uint32_t set) {
     const uint32_t pkt = set * PPW + grp;
-    const bool live = pkt < a.n;
-    process_packet<LOG2G, VERIFY>(a, pkt, live, live ? (uint64_t)pkt * a.stride : 0,
-                                  live ? a.len : 0, gl, grp * G, kc0, kc1);
+    const bool live = set < set_end && pkt < a.n;
+    return describe<DPI>(a.frames, pkt, live, live ? (uint64_t)pkt * a.stride : 0,
+                         live ? a.len : 0);
+  };
+  // (issuing the next set's first batch before finishing this one was
+  // measured: no gain at 4 KiB or 108-B frames, and register spills)
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
+    const Pkt p = make(set);
+    Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+    finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kc0, kc1);
   }
 }
 
@@ -498,12 +523,17 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
     }
     __syncthreads();
     const int nsets = (cnt + PPW - 1) / PPW;
-    for (int set = tid >> 6; set < nsets; set += 16) {
+    auto make = [&](int set) {
       const int idx = set * PPW + grp;
-      const bool live = idx < cnt;
+      const bool live = set < nsets && idx < cnt;
       const uint32_t pkt = live ? w0 + perm[idx] : 0;
-      process_packet<LOG2G, VERIFY>(a, pkt, live, live ? a.offsets[pkt] : 0,
-                                    live ? a.lens[pkt] : 0, gl, grp * G, kc0, kc1);
+      return describe<DPI>(a.frames, pkt, live, live ? a.offsets[pkt] : 0,
+                           live ? a.lens[pkt] : 0);
+    };
+    for (int set = tid >> 6; set < nsets; set += 16) {
+      const Pkt p = make(set);
+      Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kc0, kc1);
     }
     __syncthreads();
   }
