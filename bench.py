@@ -7,7 +7,8 @@ SEND_MIDDLE frames with 4 KiB payloads (4140-B wire frames, compute mode).
 With --gpus N (one process per GPU via torch.distributed.run) each rank owns its
 round-robin shard of 2^20 packets (BASELINE config 4 at N = 8: 2^23 packets in
 total); there is no data-path collective, only a gloo barrier and a max-reduce
-of the timing (weak scaling).
+of the timing (weak scaling).  --workload cfg3 / cfg5 run the other BASELINE
+configurations (mixed-MTU verify, 64-B payloads) with the same contract.
 
 Printed (rank 0): ONE JSON line with the driver's keys plus
   roofline      -- achieved algorithmic GB/s of the ICRC kernel (per-launch
@@ -38,11 +39,14 @@ HBM_PEAK_GBPS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
 
 WORKLOADS = {
-    # name: (payload bytes, packets per GPU, seed, description)
+    # name: (payload bytes (0 = mixed MTU), packets per GPU, seed, description)
     "cfg2": (4096, 1 << 20, 0x1C2C0001,
              "4 KiB-MTU RC SEND_MIDDLE frames (4140 B), ICRC compute, stride 4140"),
     "cfg5": (64, 1 << 24, 0x1C2C0005,
              "64-B payload SEND_MIDDLE-shaped frames (108 B), ICRC compute, stride 108"),
+    "cfg3": (0, 1 << 20, 0x1C2C0003,
+             "mixed-MTU {256..4096} RDMA_WRITE_MIDDLE frames packed back to back, ICRC verify "
+             "(1/1024 payload bit flips must fail, 1/1024 randomised masked fields must pass)"),
 }
 
 
@@ -61,20 +65,37 @@ def parse_args():
     return ap.parse_args()
 
 
-def cpu_baseline(buf: np.ndarray, stride: int, flen: int, n: int, gpu_icrc: np.ndarray):
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle's per-packet restatement (bench's only oracle use)
+# ---------------------------------------------------------------------------
+
+_CPU_JOB = None
+
+
+def _cpu_chunk(se):
+    import icrc_oracle as orc
+    buf, offs, lens = _CPU_JOB
+    s, e = se
+    return np.array([orc.icrc_of_frame_at(buf, int(offs[i]), int(lens[i])) for i in range(s, e)],
+                    np.uint32)
+
+
+def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: np.ndarray):
     """Per-packet zlib restatement (oracle/, the CPU "port" baseline) on this host.
 
-    Single process over the first n1 packets, then a fork pool over all n packets
+    Single process over the first ~256 MiB, then a fork pool over all packets
     (bounded: about 10 core-seconds).  Its CRCs double as a parity sample."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import multiprocessing as mp
 
     import icrc_oracle as orc
 
-    cov = flen - 4
-    n1 = min(n, max(1, (1 << 28) // flen))  # ~256 MiB single-core sample
+    n = offs.size
+    cov = lens.astype(np.int64) - 4
+    n1 = int(min(n, max(1, np.searchsorted(np.cumsum(lens, dtype=np.int64), 1 << 28))))
     t0 = time.perf_counter()
-    one = np.array([orc.icrc_of_frame_at(buf, i * stride, flen) for i in range(n1)], np.uint32)
+    one = np.array([orc.icrc_of_frame_at(buf, int(offs[i]), int(lens[i])) for i in range(n1)],
+                   np.uint32)
     t1 = time.perf_counter() - t0
     try:
         cores = len(os.sched_getaffinity(0))
@@ -82,37 +103,127 @@ def cpu_baseline(buf: np.ndarray, stride: int, flen: int, n: int, gpu_icrc: np.n
         cores = os.cpu_count() or 1
     procs = max(1, min(16, cores))
     global _CPU_JOB
-    _CPU_JOB = (buf, stride, flen)
-    chunks = [(s, min(n, s + (n + procs * 4 - 1) // (procs * 4)))
-              for s in range(0, n, (n + procs * 4 - 1) // (procs * 4))]
-    ctx = mp.get_context("fork")
+    _CPU_JOB = (buf, offs, lens)
+    step = (n + procs * 4 - 1) // (procs * 4)
+    chunks = [(s, min(n, s + step)) for s in range(0, n, step)]
     t0 = time.perf_counter()
-    with ctx.Pool(procs) as pool:
+    with mp.get_context("fork").Pool(procs) as pool:
         parts = pool.map(_cpu_chunk, chunks)
     tn = time.perf_counter() - t0
     allc = np.concatenate(parts)
-    mism = int((allc != gpu_icrc[:n]).sum()) + int((one != gpu_icrc[:n1]).sum())
+    mism = int((allc != gpu_icrc).sum()) + int((one != gpu_icrc[:n1]).sum())
+    c_all, c_one = int(cov.sum()), int(cov[:n1].sum())
     return {
-        "value": round(n * cov / tn / 2**30, 4),
+        "value": round(c_all / tn / 2**30, 4),
         "unit": "GiB/s",
         "cores": procs,
         "kind": "port",
         "sample": (f"Python zlib.crc32 restatement of BTH.compute_icrc per packet over the same "
-                   f"host frames: {n} packets on a {procs}-process fork pool "
-                   f"({tn:.2f} s); single core {n1} packets {n1 * cov / t1 / 2**30:.3f} GiB/s"),
-        "single_core_GiBps": round(n1 * cov / t1 / 2**30, 4),
+                   f"host frames: {n} packets on a {procs}-process fork pool ({tn:.2f} s); "
+                   f"single core {n1} packets {c_one / t1 / 2**30:.3f} GiB/s"),
+        "single_core_GiBps": round(c_one / t1 / 2**30, 4),
         "parity_mismatches_vs_gpu": mism,
     }
 
 
-_CPU_JOB = None
+# ---------------------------------------------------------------------------
+# Workloads
+# ---------------------------------------------------------------------------
 
 
-def _cpu_chunk(se):
-    import icrc_oracle as orc
-    buf, stride, flen = _CPU_JOB
-    s, e = se
-    return np.array([orc.icrc_of_frame_at(buf, i * stride, flen) for i in range(s, e)], np.uint32)
+class Strided:
+    """cfg2 / cfg4 / cfg5: fixed-size frames, ICRC compute."""
+
+    mode = "compute"
+
+    def __init__(self, torch, eng, dev, payload, n, seed, rank, world):
+        from roce_icrc import synth
+        self.torch, self.eng, self.n = torch, eng, n
+        self.buf, self.stride, self.flen = synth.uniform_frames(
+            n, payload, seed=seed if world == 1 else seed + rank, psn_start=rank, psn_step=world)
+        self.offs = np.arange(n, dtype=np.uint64) * self.stride
+        self.lens = np.full(n, self.flen, np.uint32)
+        self.covered = n * (self.flen - 4)
+        self.alg_bytes = n * self.flen  # C_i read + 4-B ICRC written (SURVEY.md 8(d))
+        self.d_frames = torch.from_numpy(self.buf).to(dev)
+        self.out = torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def step(self, sp):
+        self.eng.compute_strided_dev(self.d_frames, self.stride, self.flen, self.n, self.out,
+                                     stream=sp)
+
+    def upload(self, h_frames):
+        self.d_frames.copy_(h_frames, non_blocking=True)
+
+    def results(self):
+        return self.out.cpu().numpy().view(np.uint32).copy()
+
+    def lanes(self):
+        return self.eng.lanes_for_len(self.flen)
+
+    def check(self):
+        return {}
+
+
+class RaggedVerify:
+    """cfg3: mixed-MTU frames packed back to back, ICRC verify.  Trailers are
+    filled by the engine's compute path on the device (its parity is the test
+    suite's job), then 1/1024 frames get a payload bit flip (must fail) and
+    1/1024 get random masked-field values (must pass)."""
+
+    mode = "verify"
+
+    def __init__(self, torch, eng, dev, payload, n, seed, rank, world):
+        from roce_icrc import synth
+        self.torch, self.eng, self.n = torch, eng, n
+        self.buf, self.offs, self.lens = synth.mixed_mtu_frames(
+            n, seed=seed if world == 1 else seed + rank)
+        self.covered = synth.covered_bytes(self.lens)
+        self.alg_bytes = self.covered + 5 * n  # C_i + 4-B trailer read, 1-B ok flag written
+        self.d_frames = torch.from_numpy(self.buf).to(dev)
+        self.d_offs = torch.from_numpy(self.offs.view(np.int64)).to(dev)
+        self.d_lens = torch.from_numpy(self.lens.view(np.int32)).to(dev)
+        self.icrc = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        eng.compute_batch_dev(self.d_frames, self.d_offs, self.d_lens, n, self.icrc, stream=sp)
+        trail = (self.d_offs + self.d_lens.to(torch.int64) - 4)
+        idx = trail[:, None] + torch.arange(4, device=dev)[None, :]
+        self.d_frames[idx.reshape(-1)] = self.icrc.view(torch.uint8).reshape(-1)
+        rng = np.random.Generator(np.random.PCG64(seed + 17))
+        sel = rng.choice(n, size=2 * max(1, n // 1024), replace=False)
+        self.flip, self.masked = np.sort(sel[: len(sel) // 2]), np.sort(sel[len(sel) // 2:])
+        pay_off = self.offs[self.flip].astype(np.int64) + 40 + rng.integers(
+            0, self.lens[self.flip].astype(np.int64) - 44)
+        bits = torch.from_numpy(1 << rng.integers(0, 8, self.flip.size)).to(dev).to(torch.uint8)
+        p = torch.from_numpy(pay_off).to(dev)
+        self.d_frames[p] ^= bits
+        for k in (1, 8, 10, 11, 26, 27, 32):
+            p = torch.from_numpy(self.offs[self.masked].astype(np.int64) + k).to(dev)
+            v = torch.from_numpy(rng.integers(0, 256, self.masked.size).astype(np.uint8)).to(dev)
+            self.d_frames[p] = v
+        torch.cuda.synchronize(dev)
+        self.buf = self.d_frames.cpu().numpy()  # host copy with trailers + corruptions
+
+    def step(self, sp):
+        self.eng.verify_batch_dev(self.d_frames, self.d_offs, self.d_lens, self.n, self.ok,
+                                  self.icrc, stream=sp)
+
+    def upload(self, h_frames):
+        self.d_frames.copy_(h_frames, non_blocking=True)
+
+    def results(self):
+        return self.icrc.cpu().numpy().view(np.uint32).copy()
+
+    def lanes(self):
+        return "ragged default (8 at the mixed-MTU mean)"
+
+    def check(self):
+        ok = self.ok.cpu().numpy().astype(bool)
+        return {"verify_ok": int(ok.sum()), "verify_failed": int((~ok).sum()),
+                "flipped_all_failed": bool((~ok[self.flip]).all()),
+                "masked_all_passed": bool(ok[self.masked].all()),
+                "expected_failures": int(self.flip.size)}
 
 
 def main():
@@ -129,28 +240,23 @@ def main():
     if args.gpus != world and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
               file=sys.stderr)
+    # ROCE_ICRC_BENCH_DEVICE pins every rank to one device: a rehearsal of the
+    # N-rank path on a 1-GPU box (never set by the driver's scaling runs)
+    local = int(os.environ.get("ROCE_ICRC_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
-    from roce_icrc import IcrcEngine, synth
+    from roce_icrc import IcrcEngine
 
     eng = IcrcEngine(local, lanes=args.lanes)
     payload, n_default, seed, desc = WORKLOADS[args.workload]
     n = args.packets or n_default
-    # rank r owns global packets r, r+N, r+2N, ... (round robin); its payloads
-    # come from its own PCG64 stream
-    buf, stride, flen = synth.uniform_frames(
-        n, payload, seed=seed if world == 1 else seed + rank, psn_start=rank, psn_step=world)
-    cov = flen - 4
     dev = torch.device("cuda", local)
-    d_frames = torch.from_numpy(buf).to(dev)
-    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    W = (RaggedVerify if args.workload == "cfg3" else Strided)(
+        torch, eng, dev, payload, n, seed, rank, world)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    def step():
-        eng.compute_strided_dev(d_frames, stride, flen, n, out, stream=sp)
-
     for _ in range(args.warmup):
-        step()
+        W.step(sp)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -160,7 +266,7 @@ def main():
     t0 = time.perf_counter()
     for a, b in evs:
         a.record(stream)
-        step()
+        W.step(sp)
         b.record(stream)
     torch.cuda.synchronize(dev)
     t_local = time.perf_counter() - t0
@@ -171,48 +277,48 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t[0])
-    gpu_icrc = out.cpu().numpy().view(np.uint32).copy()
+    gpu_icrc = W.results()
+    checks = W.check()
 
     # STREAM-style read of the same frame buffer (measured HBM-read denominator)
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
-    nb = d_frames.numel() // 16 * 16
-    eng.stream_read_dev(d_frames, nb, sink, stream=sp)
+    nb = W.d_frames.numel() // 16 * 16
+    eng.stream_read_dev(W.d_frames, nb, sink, stream=sp)
     torch.cuda.synchronize(dev)
     se = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     srs = []
     for _ in range(5):
         se[0].record(stream)
-        eng.stream_read_dev(d_frames, nb, sink, stream=sp)
+        eng.stream_read_dev(W.d_frames, nb, sink, stream=sp)
         se[1].record(stream)
         se[1].synchronize()
         srs.append(se[0].elapsed_time(se[1]) * 1e-3)
     stream_read_gbps = nb / float(np.median(srs)) / 1e9
 
-    # host-inclusive rate: pinned H2D of the frames + kernel + D2H of the ICRCs
+    # host-inclusive rate: pinned H2D of the frames + kernel + D2H of the results
     e2e = None
     if not args.no_e2e:
-        h_pinned = torch.from_numpy(buf).pin_memory()
+        h_pinned = torch.from_numpy(W.buf).pin_memory()
         h_out = torch.empty(n, dtype=torch.int32).pin_memory()
         ts = []
         for _ in range(3):
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
-            d_frames.copy_(h_pinned, non_blocking=True)
-            step()
-            h_out.copy_(out, non_blocking=True)
+            W.upload(h_pinned)
+            W.step(sp)
+            h_out.copy_(W.out if hasattr(W, "out") else W.icrc, non_blocking=True)
             torch.cuda.synchronize(dev)
             ts.append(time.perf_counter() - t0)
-        e2e = n * cov / min(ts) / 2**30
+        e2e = W.covered / min(ts) / 2**30
         del h_pinned, h_out
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(buf, stride, flen, n, gpu_icrc)
+        cpu = cpu_baseline(W.buf, W.offs, W.lens, gpu_icrc)
 
     if rank == 0:
         mean_k = float(np.mean(kern_s))
-        alg_bytes = n * (cov + 4)  # C_i read + 4-B ICRC written
-        achieved = alg_bytes / mean_k / 1e9
+        achieved = W.alg_bytes / mean_k / 1e9
         traffic = None
         if PMC_FILE.exists():
             try:
@@ -221,7 +327,7 @@ def main():
                     traffic = pmc.get("traffic_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
-        value = world * n * cov * args.steps / t_max / 2**30
+        value = world * W.covered * args.steps / t_max / 2**30
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -237,10 +343,10 @@ def main():
             "data": "synthetic (numpy PCG64 payloads, scapy-default IPv4/UDP/BTH headers)",
             "config": {
                 "workload": f"{args.workload}: {desc}",
+                "mode": W.mode,
                 "packets_per_gpu": n,
-                "frame_bytes": flen,
-                "covered_bytes_per_packet": cov,
-                "lanes_per_packet": eng.lanes_for_len(flen),
+                "covered_bytes_per_gpu": W.covered,
+                "lanes_per_packet": args.lanes or W.lanes(),
                 "parallelism": f"{world} GPU(s), round-robin packet shards, no collective",
             },
             "roofline": {
@@ -250,12 +356,15 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
+                "alg_bytes_per_launch": W.alg_bytes,
             },
             "cpu_baseline": cpu,
             "kernel_ms_mean": round(mean_k * 1e3, 4),
             "stream_read_GBps": round(stream_read_gbps, 1),
             "end_to_end_GiBps": None if e2e is None else round(e2e, 3),
         }
+        if checks:
+            line["checks"] = checks
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
