@@ -157,12 +157,39 @@ __device__ __forceinline__ uint32_t fix_dword(uint32_t v, int k, int kub, int kb
   return v ^ ((k == 0) ? kSeedRegister : 0u);
 }
 
-// Head fix-up of one chunk (iterations j < jh): zero dwords before the frame,
-// apply masks and seed, and keep the raw header dwords 0 and 2.
+// 4-way select of a chunk's dword t (t outside 0..3 keeps `dflt`).
+__device__ __forceinline__ uint32_t pick4(const u32x4& w, int t, uint32_t dflt) {
+  const uint32_t lo = (t & 1) ? w.y : w.x;
+  const uint32_t hi = (t & 1) ? w.w : w.z;
+  const uint32_t v = (t & 2) ? hi : lo;
+  return ((unsigned)t < 4u) ? v : dflt;
+}
+
+// Head fix-up of one chunk (iterations j < jh) for IHL-5 frames: zero dwords
+// before the frame, apply masks and seed, and keep the raw header dwords 0
+// and 2.  The per-dword (AND, OR, XOR) triple comes from a 13-entry table in
+// LDS indexed by clamp(k + 3, 0, 12) (entries 0-2: k < 0, 3-11: k = 0..8,
+// 12: k > 8), one ds_read_b128 and two VALU per dword.
+__device__ __forceinline__ void fix_chunk5(u32x4& w, int kb, uint32_t lut, uint32_t& h0,
+                                           uint32_t& h2) {
+  h0 = pick4(w, -kb, h0);
+  h2 = pick4(w, 2 - kb, h2);
+  u32x4 e;
+#define RICRC_FIX(c, t)                                                            \
+  e = *(const lds_u32x4*)(uintptr_t)(lut + 16u * (uint32_t)min(max(kb + (t) + 3, 0), 12)); \
+  w.c = ((w.c & e.x) | e.y) ^ e.z;
+  RICRC_FIX(x, 0)
+  RICRC_FIX(y, 1)
+  RICRC_FIX(z, 2)
+  RICRC_FIX(w, 3)
+#undef RICRC_FIX
+}
+
+// General-IHL fix-up (slow path for frames with IPv4 options).
 __device__ __forceinline__ void fix_chunk(u32x4& w, int kb, int kub, int kbb, uint32_t& h0,
                                           uint32_t& h2) {
-  h0 = (kb == 0) ? w.x : (kb == -1) ? w.y : (kb == -2) ? w.z : (kb == -3) ? w.w : h0;
-  h2 = (kb == 2) ? w.x : (kb == 1) ? w.y : (kb == 0) ? w.z : (kb == -1) ? w.w : h2;
+  h0 = pick4(w, -kb, h0);
+  h2 = pick4(w, 2 - kb, h2);
   w.x = (kb + 0 < 0) ? 0u : fix_dword(w.x, kb + 0, kub, kbb);
   w.y = (kb + 1 < 0) ? 0u : fix_dword(w.y, kb + 1, kub, kbb);
   w.z = (kb + 2 < 0) ? 0u : fix_dword(w.z, kb + 2, kub, kbb);
@@ -287,6 +314,15 @@ __device__ __forceinline__ void stage_tables(const IcrcArgs& a, int tid) {
   }
   const uint32_t* gc = a.tables + kNumMainSets * 1024;
   for (int i = tid; i < NCOMB * 1024; i += 1024) lds_wr(kLdsMain + 4u * i, gc[i]);
+  if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
+    const int k = tid - 3;
+    const uint32_t lut = kLdsMain + 4096u * NCOMB;
+    const uint32_t andm = k < 0 ? 0u : ~0u;
+    const uint32_t orm = k == 0 ? 0x0000FF00u : k == 2 ? 0xFFFF00FFu : k == 6 ? 0xFFFF0000u
+                         : k == 8 ? 0x000000FFu : 0u;
+    const uint32_t xorm = k == 0 ? kSeedRegister : 0u;
+    *(lds_u32x4*)(uintptr_t)(lut + 16u * tid) = u32x4{andm, orm, xorm, 0u};
+  }
 }
 
 // A packet's first batch of loads: head chunks, the first body block and the
@@ -326,6 +362,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   constexpr int U = kUnroll;
+  constexpr uint32_t kLut = kLdsMain + 4096u * (1 + LOG2G);
   // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
   // U (the first block holds the remainder), then the last one (J-1), which
   // skips columns past the end and may also need the fix-ups.
@@ -339,7 +376,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < jhh; ++j) {
     u32x4 w = (j == 0) ? b.wh0 : (j == 1) ? b.wh1 : load_chunk<G>(p, j, gl);
-    fix_chunk(w, DPI * j + 4 * gl - p.S, 6, 8, h0, h2);
+    fix_chunk5(w, DPI * j + 4 * gl - p.S, kLut, h0, h2);
     fold(A, w, kc0, kc1);
   }
   // body blocks, ping-pong between b.cur and nxt (no register copies)
@@ -369,7 +406,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   {
     u32x4 w = b.wl;
     const int kb = DPI * JL + 4 * gl - p.S;
-    if (JL < p.jh) fix_chunk(w, kb, 6, 8, h0, h2);
+    if (JL < p.jh) fix_chunk5(w, kb, kLut, h0, h2);
     fold_last(A, w, kb, p.n, kc0, kc1);
   }
 
@@ -449,7 +486,7 @@ __global__ void __launch_bounds__(1024, 1) icrc_strided_kernel(IcrcArgs a) {
 template <int LOG2G>
 struct RaggedLds {
   static constexpr int kNComb = 1 + LOG2G;
-  static constexpr uint32_t kBase = kLdsMain + 4096u * kNComb;
+  static constexpr uint32_t kBase = kLdsMain + 4096u * kNComb + 256u;  // after the fix-up LUT
   static constexpr int kBuckets = 128;
   static constexpr uint32_t kHist = kBase;               // kBuckets x u32 counts / cursors
   static constexpr uint32_t kPerm = kBase + 4 * kBuckets;  // window x u16 local indices
@@ -583,7 +620,7 @@ kernel_fn select_kernel(int log2g, bool ragged, bool verify) {
 }
 
 size_t lds_bytes(int log2g, bool ragged) {
-  if (!ragged) return kLdsMain + 4096u * (1 + log2g);
+  if (!ragged) return kLdsMain + 4096u * (1 + log2g) + 256u;
   switch (log2g) {
     case 0: return RaggedLds<0>::kBytes;
     case 1: return RaggedLds<1>::kBytes;
