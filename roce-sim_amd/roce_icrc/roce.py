@@ -569,3 +569,31 @@ def verify_frames(frames: list[bytes]) -> np.ndarray:
         offs[1:] = np.cumsum(lens[:-1])
     ok, _, _ = get_engine().verify_batch(np.frombuffer(b"".join(frames), np.uint8), offs, lens)
     return ok
+
+
+def recv_datagrams(datagrams: list[bytes], qpn: Optional[int] = None):
+    """Receive side for raw IPv4 datagrams (e.g. from an AF_INET/SOCK_RAW UDP
+    socket): verify every ICRC in one GPU call, drop the failures (as Linux
+    rxe does), and return ``(packets, dropped)`` where ``packets`` are the
+    ``BTH`` objects the reference would dissect from the UDP payload
+    (src/roce_v2.py:347-350, src/roce_rq.py:899-901) and ``dropped`` the
+    indices of datagrams whose ICRC did not match.  ``qpn`` skips packets for
+    other QPs like ``RoCEv2.recv_pkts`` (src/roce_v2.py:357-362).
+
+    The reference's UDP socket never sees the IPv4 header the ICRC covers
+    (SURVEY.md section 0.2), so this check sits one layer lower, in front of
+    ``QP.recv_pkt`` / ``verify_pkt_head`` (src/roce_v2.py:171-192)."""
+    if not datagrams:
+        return [], []
+    ok = verify_frames(datagrams)
+    packets, dropped = [], []
+    for i, (d, good) in enumerate(zip(datagrams, ok)):
+        if not good:
+            dropped.append(i)
+            continue
+        ihl = 4 * (d[0] & 0xF)
+        bth = BTH(d[ihl + 8:])
+        if qpn is not None and bth.dqpn != qpn:
+            continue
+        packets.append(bth)
+    return packets, dropped

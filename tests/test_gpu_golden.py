@@ -68,3 +68,17 @@ def test_emit_batch_and_verify(engine):
     bad[3] = bad[3][:50] + bytes([bad[3][50] ^ 0x10]) + bad[3][51:]
     ok = R.verify_frames(bad)
     assert not ok[3] and ok.sum() == len(frames) - 1
+
+
+def test_recv_datagrams_drops_bad_icrc(engine):
+    R.set_engine(engine)
+    pkts = [R.l3_packet(R.BTH(opcode=0x01, psn=i, dqpn=0x30 + (i % 2)) / R.Raw(load=bytes([i]) * 64),
+                        dst="10.0.0.2", sport=7, src="10.0.0.1") for i in range(10)]
+    frames = R.emit_batch(pkts)
+    frames[4] = frames[4][:60] + bytes([frames[4][60] ^ 4]) + frames[4][61:]
+    got, dropped = R.recv_datagrams(frames)
+    assert dropped == [4] and len(got) == 9
+    assert [b.psn for b in got] == [0, 1, 2, 3, 5, 6, 7, 8, 9]
+    assert got[0][R.Raw].load == bytes([0]) * 64
+    got, dropped = R.recv_datagrams(frames, qpn=0x31)
+    assert [b.psn for b in got] == [1, 3, 5, 7, 9]
