@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define RICRC_ABI_VERSION 1
+#define RICRC_ABI_VERSION 2
 
 /* call-level return codes */
 #define RICRC_OK 0
@@ -134,7 +134,93 @@ int ricrc_verify_strided_dev(ricrc_ctx* ctx, const uint8_t* d_frames, uint64_t s
                              uint32_t* d_icrc /* nullable */, uint8_t* d_status /* nullable */,
                              void* stream);
 
+/* ---- MR -> packet segmentation fused with the ICRC (device-built frames) --
+ *
+ *   reference                                        replaced by
+ *   -----------------------------------------------  -----------------------------
+ *   TXLogic.process_send_req    src/roce_sq.py:1243   one ricrc_seg_wr of op SEND*
+ *   TXLogic.process_write_req   src/roce_sq.py:1323   one ricrc_seg_wr of op RDMA_WRITE*
+ *   ReadReqCtx.commit           src/roce_rq.py:388    one ricrc_seg_wr of op READ_RESPONSE
+ *   Util.compute_wr_pkt_num     src/roce_util.py:183  ricrc_segment_plan
+ *   Util.add_padding_if_needed  src/roce_util.py:187  (in the kernel)
+ *   IP()/UDP() wrap of send_ip_pkt / send_pkt         (in the kernel: IPv4 id 1, ttl 64,
+ *     src/roce_sq.py:1186-1197, src/roce_rq.py:705-731  header checksum, UDP dport 4791,
+ *                                                       UDP checksum over the final bytes)
+ *   BTH.compute_icrc            src/roce.py:192       (in the kernel, same register fold)
+ *
+ * Packet k (0-based) of a WR of n = compute_wr_pkt_num(length, pmtu) packets
+ * gets PSN (psn + k) mod 2^24, the FIRST/MIDDLE/LAST/ONLY opcode of its
+ * position, the extension headers of that opcode (RETH on WRITE FIRST/ONLY,
+ * RETHImmDt on WRITE_ONLY_WITH_IMM, ImmDt on *_WITH_IMM last, IETH on
+ * SEND_*_WITH_INV last, AETH(ACK, 31, msn) on READ_RESPONSE FIRST/LAST/ONLY),
+ * the MR bytes [mr_offset + k*pmtu, ...) as payload (none when length == 0),
+ * zero padding to 4 bytes with BTH.padcount, ackreq = SIGNALED and solicited
+ * = SOLICITED on the last packet only (solicited only for SEND* and
+ * RDMA_WRITE_WITH_IMM, as the reference), and its ICRC.
+ *
+ * Output: packet p (WR order, packet order) is the wire frame at
+ * frames + p * slot_bytes, lens[p] bytes long (0 with status
+ * RICRC_PKT_SEG_BAD when its WR is invalid); slot bytes past the frame end, up
+ * to the next 16-byte boundary, are written as zeros.
+ */
+#define RICRC_SEG_SEND 0
+#define RICRC_SEG_SEND_WITH_IMM 1
+#define RICRC_SEG_SEND_WITH_INV 2
+#define RICRC_SEG_RDMA_WRITE 3
+#define RICRC_SEG_RDMA_WRITE_WITH_IMM 4
+#define RICRC_SEG_READ_RESPONSE 5
+#define RICRC_SEG_SIGNALED 0x1  /* SEND_FLAGS.SIGNALED (src/roce_sq.py:1256)  */
+#define RICRC_SEG_SOLICITED 0x2 /* SEND_FLAGS.SOLICITED (src/roce_sq.py:1257) */
+#define RICRC_PKT_SEG_BAD 0x20  /* WR op unknown, MR range out of bounds, or packet not covered */
+
+typedef struct ricrc_seg_wr {
+  uint64_t mr_offset; /* message start: byte offset into the MR buffer (any alignment) */
+  uint64_t remote_va; /* RETH.va (RDMA WRITE)                                         */
+  uint32_t length;    /* message bytes; 0 = one packet without payload                */
+  uint32_t psn;       /* PSN of the first packet (24 bits)                            */
+  uint32_t dqpn;      /* BTH.dqpn (24 bits)                                           */
+  uint32_t src_ip;    /* IPv4 source as an integer (10.1.1.48 = 0x0A010130)           */
+  uint32_t dst_ip;    /* IPv4 destination                                             */
+  uint32_t rkey;      /* RETH.rkey (RDMA WRITE)                                       */
+  uint32_t imm;       /* ImmDt.data (*_WITH_IMM) or IETH.rkey (SEND_WITH_INV)         */
+  uint32_t msn;       /* AETH.msn (READ_RESPONSE, 24 bits)                            */
+  uint16_t sport;     /* UDP source port = the sender's QPN (src/roce_sq.py:1191)     */
+  uint8_t op;         /* RICRC_SEG_*                                                  */
+  uint8_t flags;      /* RICRC_SEG_SIGNALED | RICRC_SEG_SOLICITED                     */
+  uint32_t first_pkt; /* index of the WR's first packet; set by ricrc_segment_plan    */
+  uint32_t reserved[2];
+} ricrc_seg_wr; /* 64 bytes */
+
+/* Host-only planning (no GPU): checks every WR's op, fills wrs[i].first_pkt
+ * with the running packet count, returns the total packets and the slot size
+ * (the largest frame for `pmtu`, rounded up to 256 bytes).  pmtu: 256, 512,
+ * 1024, 2048 or 4096 (IB MTU). */
+int ricrc_segment_plan(ricrc_seg_wr* wrs, uint32_t nwr, uint32_t pmtu, uint32_t* npkts_out,
+                       uint32_t* slot_bytes_out);
+/* Host buffers, synchronous: MR copied to the device, frames built and
+ * ICRC'd there, frames/lens/ICRCs copied back.  `wrs` must be planned.
+ * frames_bytes >= npkts * slot_bytes. */
+int ricrc_segment(ricrc_ctx* ctx, const uint8_t* mr, size_t mr_bytes, const ricrc_seg_wr* wrs,
+                  uint32_t nwr, uint32_t pmtu, uint8_t* frames, size_t frames_bytes,
+                  uint32_t* lens, uint32_t* icrc_out /* nullable */,
+                  uint8_t* status_out /* nullable */);
+/* Device-resident, asynchronous on `stream`: d_mr (mr_bytes) and d_wrs
+ * (planned on the host, then copied) are device pointers; frames go to
+ * d_frames + p * slot_bytes (slot_bytes: multiple of 256, >= the plan's;
+ * d_frames 256-byte aligned).  d_lens doubles as the packet -> WR map while
+ * the call runs. */
+int ricrc_segment_dev(ricrc_ctx* ctx, const uint8_t* d_mr, uint64_t mr_bytes,
+                      const ricrc_seg_wr* d_wrs, uint32_t nwr, uint32_t pmtu, uint32_t npkts,
+                      uint8_t* d_frames, uint32_t slot_bytes, uint32_t* d_lens,
+                      uint32_t* d_icrc /* nullable */, uint8_t* d_status /* nullable */,
+                      void* stream);
+
 /* ---- measurement -------------------------------------------------------- */
+/* STREAM-style copy of `bytes` (multiple of 16) from d_src to d_dst with
+ * 16-B loads and stores: the read+write denominator of the segmentation
+ * roofline. */
+int ricrc_stream_copy_dev(ricrc_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, uint64_t bytes,
+                          void* stream);
 /* STREAM-style read of `bytes` (multiple of 16) from d_buf with 16-B coalesced
  * loads, XOR-folded into d_sink[0]: the HBM-read denominator for the roofline. */
 int ricrc_stream_read_dev(ricrc_ctx* ctx, const uint8_t* d_buf, uint64_t bytes,

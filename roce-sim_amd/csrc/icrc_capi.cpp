@@ -34,6 +34,11 @@ struct ricrc_ctx {
   uint8_t* d_status = nullptr;
   uint8_t* d_ok = nullptr;
   size_t pkt_cap = 0;
+  // segmentation scratch (host-buffer entry point)
+  uint8_t* d_mr = nullptr;
+  size_t mr_cap = 0;
+  ricrc_seg_wr* d_wrs = nullptr;
+  size_t wr_cap = 0;
 };
 
 namespace {
@@ -179,6 +184,63 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
   return RICRC_OK;
 }
 
+// Segmentation: the largest frame of a PMTU (IPv4 20 + UDP 8 + BTH 12 +
+// RETHImmDt 20 + payload + ICRC 4), rounded up to 256 bytes so every slot
+// starts at grid column 0 for up to 16 lanes per packet.
+uint32_t seg_slot_bytes(uint32_t pmtu) { return (60u + pmtu + 4u + 255u) & ~255u; }
+
+bool valid_pmtu(uint32_t pmtu) {
+  return pmtu == 256 || pmtu == 512 || pmtu == 1024 || pmtu == 2048 || pmtu == 4096;
+}
+
+// Lanes per packet for segmentation (1 lane is not instantiated: the UDP
+// checksum chunk and the header need G >= 2; G <= 16 keeps the slot grid).
+int seg_log2g(const ricrc_ctx* c, uint32_t pmtu) {
+  int l = c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(seg_slot_bytes(pmtu) - 192u);
+  return l < 1 ? 1 : l > 4 ? 4 : l;
+}
+
+int seg_ensure(ricrc_ctx* c, size_t mr_bytes, uint32_t nwr) {
+  if (mr_bytes > c->mr_cap) {
+    (void)hipFree(c->d_mr);
+    c->d_mr = nullptr;
+    c->mr_cap = 0;
+    const size_t cap = mr_bytes < 4096 ? 4096 : mr_bytes;
+    HIP_TRY(hipMalloc(&c->d_mr, cap));
+    c->mr_cap = cap;
+  }
+  if (nwr > c->wr_cap) {
+    (void)hipFree(c->d_wrs);
+    c->d_wrs = nullptr;
+    c->wr_cap = 0;
+    const size_t cap = nwr < 256 ? 256 : nwr;
+    HIP_TRY(hipMalloc(&c->d_wrs, cap * sizeof(ricrc_seg_wr)));
+    c->wr_cap = cap;
+  }
+  return RICRC_OK;
+}
+
+int seg_launch(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes, const ricrc_seg_wr* d_wrs,
+               uint32_t nwr, uint32_t pmtu, uint32_t npkts, uint8_t* d_frames, uint32_t slot,
+               uint32_t* d_lens, uint32_t* d_icrc, uint8_t* d_status, hipStream_t s) {
+  ricrc::SegArgs a{};
+  a.mr = d_mr;
+  a.mr_bytes = mr_bytes;
+  a.wrs = d_wrs;
+  a.nwr = nwr;
+  a.pmtu = pmtu;
+  a.npkts = npkts;
+  a.frames = d_frames;
+  a.slot = slot;
+  a.lens = d_lens;
+  a.icrc_out = d_icrc;
+  a.status_out = d_status;
+  a.tables = c->d_tables;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ricrc::launch_segment(a, seg_log2g(c, pmtu), c->num_cus, s));
+  return RICRC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -247,6 +309,8 @@ void ricrc_ctx_destroy(ricrc_ctx* c) {
   (void)hipFree(c->d_icrc);
   (void)hipFree(c->d_status);
   (void)hipFree(c->d_ok);
+  (void)hipFree(c->d_mr);
+  (void)hipFree(c->d_wrs);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -422,6 +486,84 @@ int ricrc_stream_read_dev(ricrc_ctx* c, const uint8_t* d_buf, uint64_t bytes, ui
   if (!c || !d_buf || !d_sink || (bytes & 15)) return RICRC_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(ricrc::launch_stream_read(d_buf, bytes, d_sink, c->num_cus, pick_stream(c, stream)));
+  return RICRC_OK;
+}
+
+int ricrc_segment_plan(ricrc_seg_wr* wrs, uint32_t nwr, uint32_t pmtu, uint32_t* npkts_out,
+                       uint32_t* slot_bytes_out) {
+  if ((nwr && !wrs) || !npkts_out || !valid_pmtu(pmtu)) return RICRC_EINVAL;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nwr; ++i) {
+    if (wrs[i].op > RICRC_SEG_READ_RESPONSE) return RICRC_EINVAL;
+    wrs[i].first_pkt = (uint32_t)total;
+    // Util.compute_wr_pkt_num (src/roce_util.py:183-185)
+    total += wrs[i].length ? ((uint64_t)wrs[i].length + pmtu - 1) / pmtu : 1;
+    if (total > 0xFFFFFFFFull) return RICRC_EINVAL;
+  }
+  *npkts_out = (uint32_t)total;
+  if (slot_bytes_out) *slot_bytes_out = seg_slot_bytes(pmtu);
+  return RICRC_OK;
+}
+
+int ricrc_segment(ricrc_ctx* c, const uint8_t* mr, size_t mr_bytes, const ricrc_seg_wr* wrs,
+                  uint32_t nwr, uint32_t pmtu, uint8_t* frames, size_t frames_bytes,
+                  uint32_t* lens, uint32_t* icrc_out, uint8_t* status_out) {
+  if (!c || (mr_bytes && !mr) || (nwr && !wrs) || !valid_pmtu(pmtu)) return RICRC_EINVAL;
+  // re-plan a copy: the caller's first_pkt must match, every WR must lie in the MR
+  std::vector<ricrc_seg_wr> plan(wrs, wrs + nwr);
+  uint32_t npkts = 0, slot = 0;
+  int rc = ricrc_segment_plan(plan.data(), nwr, pmtu, &npkts, &slot);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < nwr; ++i)
+    if (plan[i].first_pkt != wrs[i].first_pkt || wrs[i].mr_offset > mr_bytes ||
+        wrs[i].length > mr_bytes - wrs[i].mr_offset)
+      return RICRC_EINVAL;
+  if (npkts == 0) return RICRC_OK;
+  if (!frames || !lens || frames_bytes < (size_t)npkts * slot) return RICRC_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  rc = seg_ensure(c, mr_bytes, nwr);
+  if (rc) return rc;
+  rc = ensure_frames(c, (size_t)npkts * slot);
+  if (rc) return rc;
+  rc = ensure_pkts(c, npkts);
+  if (rc) return rc;
+  if (mr_bytes) HIP_TRY(hipMemcpyAsync(c->d_mr, mr, mr_bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_wrs, plan.data(), nwr * sizeof(ricrc_seg_wr), hipMemcpyHostToDevice,
+                         c->stream));
+  rc = seg_launch(c, c->d_mr, mr_bytes, c->d_wrs, nwr, pmtu, npkts, c->d_frames, slot, c->d_lens,
+                  c->d_icrc, c->d_status, c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(frames, c->d_frames, (size_t)npkts * slot, hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipMemcpyAsync(lens, c->d_lens, npkts * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         c->stream));
+  if (icrc_out)
+    HIP_TRY(hipMemcpyAsync(icrc_out, c->d_icrc, npkts * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           c->stream));
+  if (status_out)
+    HIP_TRY(hipMemcpyAsync(status_out, c->d_status, npkts, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RICRC_OK;
+}
+
+int ricrc_segment_dev(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes,
+                      const ricrc_seg_wr* d_wrs, uint32_t nwr, uint32_t pmtu, uint32_t npkts,
+                      uint8_t* d_frames, uint32_t slot_bytes, uint32_t* d_lens, uint32_t* d_icrc,
+                      uint8_t* d_status, void* stream) {
+  if (!c || !valid_pmtu(pmtu) || (nwr && !d_wrs) || (mr_bytes && !d_mr)) return RICRC_EINVAL;
+  if (npkts == 0) return RICRC_OK;
+  if (!d_frames || !d_lens || (slot_bytes & 255u) || slot_bytes < seg_slot_bytes(pmtu) ||
+      ((uintptr_t)d_frames & 255u))
+    return RICRC_EINVAL;
+  return seg_launch(c, d_mr, mr_bytes, d_wrs, nwr, pmtu, npkts, d_frames, slot_bytes, d_lens,
+                    d_icrc, d_status, pick_stream(c, stream));
+}
+
+int ricrc_stream_copy_dev(ricrc_ctx* c, const uint8_t* d_src, uint8_t* d_dst, uint64_t bytes,
+                          void* stream) {
+  if (!c || !d_src || !d_dst || (bytes & 15)) return RICRC_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ricrc::launch_stream_copy(d_src, d_dst, bytes, c->num_cus, pick_stream(c, stream)));
   return RICRC_OK;
 }
 

@@ -1,0 +1,184 @@
+// Device-side building blocks shared by the ICRC kernels (icrc_kernels.hip)
+// and the segmentation kernel (segment_kernels.hip): LDS access, the
+// (P, T) column fold, the group combine, header masks and the LDS staging of
+// the GF(2) tables.  See the header comment of icrc_kernels.hip for the
+// algebra and the LDS layout.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf2.hpp"
+#include "icrc_internal.hpp"
+
+namespace ricrc {
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+constexpr uint32_t kLdsMain = 131072;
+#ifndef RICRC_UNROLL
+#define RICRC_UNROLL 4
+#endif
+constexpr int kUnroll = RICRC_UNROLL;  // iterations per body block (dwordx4 loads in flight per lane)
+
+__device__ __forceinline__ uint32_t lds_rd(uint32_t byte_addr) {
+  return *(const lds_u32*)(uintptr_t)byte_addr;
+}
+__device__ __forceinline__ void lds_wr(uint32_t byte_addr, uint32_t v) {
+  *(lds_u32*)(uintptr_t)byte_addr = v;
+}
+__device__ __forceinline__ void lds_wr4(uint32_t byte_addr, uint32_t v) {
+  *(lds_u32x4*)(uintptr_t)byte_addr = u32x4{v, v, v, v};
+}
+
+__device__ __forceinline__ uint32_t ldg32(const uint8_t* p) {
+  return *(const uint32_t*)p;
+}
+// 16-byte streaming load from a 4-byte-aligned address (frames are only dword
+// aligned; gfx950 runs global loads in unaligned mode).  Non-temporal: every
+// frame byte is read exactly once (measured +8-10 % HBM read rate on MI355X).
+__device__ __forceinline__ u32x4 ldg128(const uint8_t* p) {
+  return __builtin_nontemporal_load((const u32x4*)p);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Mul(m)(x) from an unreplicated combine set at LDS byte address `base`.
+__device__ __forceinline__ uint32_t mul_comb(uint32_t x, uint32_t base) {
+  const uint32_t t0 = lds_rd(base + ((x << 2) & 0x3FCu));
+  const uint32_t t1 = lds_rd(base + 1024 + ((x >> 6) & 0x3FCu));
+  const uint32_t t2 = lds_rd(base + 2048 + ((x >> 14) & 0x3FCu));
+  const uint32_t t3 = lds_rd(base + 3072 + ((x >> 22) & 0x3FCu));
+  return xor3(t0, t1, t2) ^ t3;
+}
+
+// Masked dword k: TOS (k 0), TTL + IP checksum (k 2), UDP checksum (kub),
+// BTH fecn|becn|resv6 (kbb); the FF x 8 prefix enters as the register
+// 0xDEBB20E3 XORed into dword 0.
+__device__ __forceinline__ uint32_t fix_dword(uint32_t v, int k, int kub, int kbb) {
+  v |= (k == 0 ? 0x0000FF00u : 0u) | (k == 2 ? 0xFFFF00FFu : 0u) | (k == kub ? 0xFFFF0000u : 0u) |
+       (k == kbb ? 0x000000FFu : 0u);
+  return v ^ ((k == 0) ? kSeedRegister : 0u);
+}
+
+// 4-way select of a chunk's dword t (t outside 0..3 keeps `dflt`).
+__device__ __forceinline__ uint32_t pick4(const u32x4& w, int t, uint32_t dflt) {
+  const uint32_t lo = (t & 1) ? w.y : w.x;
+  const uint32_t hi = (t & 1) ? w.w : w.z;
+  const uint32_t v = (t & 2) ? hi : lo;
+  return ((unsigned)t < 4u) ? v : dflt;
+}
+
+// Fold the group's 4G column registers into the packet CRC register.  The
+// packet ends at column r of its last iteration, so column c is off by
+// x^(32 ((c - r) mod DPI)) (columns that skipped the last iteration are one
+// iteration early, which the modulus absorbs): rotate the columns by r
+// (in-lane select + ds_bpermute), then R = sum_c' Mul(-32 c')(V_c'), as
+// three in-lane Horner steps with Mul(-32) and log2 G butterfly levels with
+// Mul(-128 * 2^l).
+template <int LOG2G>
+__device__ __forceinline__ uint32_t combine(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                           int r, int gl, int base) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
+  const int rr = r & (DPI - 1);
+  const int q = rr >> 2, m = rr & 3;
+  const uint32_t v0 = m == 0 ? a0 : m == 1 ? a1 : m == 2 ? a2 : a3;
+  const uint32_t v1 = m == 0 ? a1 : m == 1 ? a2 : m == 2 ? a3 : a0;
+  const uint32_t v2 = m == 0 ? a2 : m == 1 ? a3 : m == 2 ? a0 : a1;
+  const uint32_t v3 = m == 0 ? a3 : m == 1 ? a0 : m == 2 ? a1 : a2;
+  uint32_t V0 = v0, V1 = v1, V2 = v2, V3 = v3;
+  if constexpr (G > 1) {
+    const int s0 = base + ((gl + q) & (G - 1));
+    const int s1 = base + ((gl + q + 1) & (G - 1));
+    V0 = (uint32_t)__shfl((int)v0, s0, 64);
+    V1 = (uint32_t)__shfl((int)v1, m >= 3 ? s1 : s0, 64);
+    V2 = (uint32_t)__shfl((int)v2, m >= 2 ? s1 : s0, 64);
+    V3 = (uint32_t)__shfl((int)v3, m >= 1 ? s1 : s0, 64);
+  }
+  uint32_t B = mul_comb(V3, kLdsMain) ^ V2;
+  B = mul_comb(B, kLdsMain) ^ V1;
+  B = mul_comb(B, kLdsMain) ^ V0;
+#pragma unroll
+  for (int l = 0; l < LOG2G; ++l) {
+    const uint32_t mm = mul_comb(B, kLdsMain + 4096u * (1 + l));
+    const uint32_t t = ((gl >> l) & 1) ? mm : B;
+    B = t ^ (uint32_t)__shfl_xor((int)t, 1 << l, 64);
+  }
+  return B;
+}
+
+// Column registers are kept as a pair (P, T) whose XOR is the CRC register:
+// P = t0 ^ t1 ^ t2 and T = t3 of the last four lookups.  Absorbing the next
+// dword is then ONE v_bitop3 (P ^ T ^ w), four v_perm address builds, four
+// conflict-free ds_read_b32 and one more v_bitop3: 6 VALU per dword.
+struct Col {
+  uint32_t P[4], T[4];
+};
+
+__device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w, uint32_t kc0,
+                                       uint32_t kc1) {
+#ifdef RICRC_ABLATE_FOLD  // diagnostic build only: loads kept, table folding removed
+  P ^= w;
+#else
+  const uint32_t x = xor3(P, T, w);
+  const uint32_t a0 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, kc1, 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, kc1, 0x0C020700u);
+  P = xor3(lds_rd(a0), lds_rd(a1 + 128), lds_rd(a2));
+  T = lds_rd(a3 + 128);
+#endif
+}
+
+__device__ __forceinline__ void fold(Col& c, const u32x4& w, uint32_t kc0, uint32_t kc1) {
+  absorb(c.P[0], c.T[0], w.x, kc0, kc1);
+  absorb(c.P[1], c.T[1], w.y, kc0, kc1);
+  absorb(c.P[2], c.T[2], w.z, kc0, kc1);
+  absorb(c.P[3], c.T[3], w.w, kc0, kc1);
+}
+
+// The packet's last iteration: columns past the end (k >= n) keep their register.
+__device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n, uint32_t kc0,
+                                          uint32_t kc1) {
+  Col f = c;
+  fold(f, w, kc0, kc1);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    c.P[t] = (kb + t < n) ? f.P[t] : c.P[t];
+    c.T[t] = (kb + t < n) ? f.T[t] : c.T[t];
+  }
+}
+
+// LDS staging of the folding tables (every kernel, once per workgroup).
+template <int LOG2G>
+__device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
+  constexpr int NCOMB = 1 + LOG2G;
+  const uint32_t* gm = tables + LOG2G * 1024;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = tid + r * 1024;  // 8192 16-byte quads
+    const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
+    lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16),
+            gm[tab * 256 + e]);
+  }
+  const uint32_t* gc = tables + kNumMainSets * 1024;
+  for (int i = tid; i < NCOMB * 1024; i += 1024) lds_wr(kLdsMain + 4u * i, gc[i]);
+  if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
+    const int k = tid - 3;
+    const uint32_t lut = kLdsMain + 4096u * NCOMB;
+    const uint32_t andm = k < 0 ? 0u : ~0u;
+    const uint32_t orm = k == 0 ? 0x0000FF00u : k == 2 ? 0xFFFF00FFu : k == 6 ? 0xFFFF0000u
+                         : k == 8 ? 0x000000FFu : 0u;
+    const uint32_t xorm = k == 0 ? kSeedRegister : 0u;
+    *(lds_u32x4*)(uintptr_t)(lut + 16u * tid) = u32x4{andm, orm, xorm, 0u};
+  }
+}
+
+}  // namespace
+}  // namespace ricrc

@@ -42,3 +42,31 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink
 hipError_t prepare_kernels();
 
 }  // namespace ricrc
+
+struct ricrc_seg_wr;  // include/roce_icrc.h
+
+namespace ricrc {
+
+struct SegArgs {
+  const uint8_t* mr;
+  uint64_t mr_bytes;
+  const ::ricrc_seg_wr* wrs;
+  uint32_t nwr;
+  uint32_t pmtu;
+  uint32_t npkts;
+  uint8_t* frames;
+  uint32_t slot;
+  uint32_t* lens;  // packet -> WR map on entry (seg map kernel), frame lengths on exit
+  uint32_t* icrc_out;   // nullable
+  uint8_t* status_out;  // nullable
+  const uint32_t* tables;
+};
+
+// Enqueues the packet -> WR map kernel and the segmentation kernel.
+hipError_t launch_segment(const SegArgs& a, int log2g, int num_cus, hipStream_t stream);
+
+// Enqueues the STREAM-style copy kernel (segmentation roofline denominator).
+hipError_t launch_stream_copy(const uint8_t* src, uint8_t* dst, uint64_t bytes, int num_cus,
+                              hipStream_t stream);
+
+}  // namespace ricrc

@@ -1,0 +1,477 @@
+// MR -> packet segmentation fused with the ICRC, for MI355X (gfx950).
+//
+// Builds, on the GPU and straight from the memory region, every wire frame
+// roce-sim's requester and responder emit for a batch of work requests:
+// TXLogic.process_send_req (src/roce_sq.py:1243-1321), process_write_req
+// (src/roce_sq.py:1323-1411) and ReadReqCtx.commit (src/roce_rq.py:388-438),
+// each packet wrapped in IPv4/UDP as send_ip_pkt / send_pkt do
+// (src/roce_sq.py:1186-1197, src/roce_rq.py:705-731), padded as
+// Util.add_padding_if_needed (src/roce_util.py:187-199), with its IPv4 header
+// checksum, its ICRC (BTH.compute_icrc, src/roce.py:192-223) and its UDP
+// checksum (scapy UDP.post_build, which runs after the ICRC is in place).
+//
+// One pass: a group of G lanes owns one packet; the packet's frame is laid on
+// the same dword grid as the ICRC kernel (icrc_kernels.hip) with the frame
+// starting at grid column 0 (slots are 256-byte aligned), so in iteration j
+// lane i produces the 16 frame bytes of dwords 4Gj + 4i .. +3: header dwords
+// from the WR descriptor, payload dwords with one (unaligned) 16-byte MR load,
+// stores them with one aligned 16-byte store and folds them into its four CRC
+// columns and its UDP one's-complement sum in registers.  The frame is read
+// from the MR once and written once; nothing is read back.  Two chunks per
+// packet are held back until the group has combined its CRC and checksum: the
+// one holding the UDP checksum (dword 6) and the one holding the ICRC slot.
+//
+// Packet -> WR: a first small kernel writes each packet's WR index into the
+// `lens` output array (one workgroup per WR); the segmentation kernel reads
+// that entry and overwrites it with the frame length.
+#include "icrc_device.hpp"
+#include "roce_icrc.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace ricrc {
+
+namespace {
+
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+
+constexpr int kSegUnroll = 4;          // body iterations (16-byte MR loads per lane) in flight
+constexpr uint32_t kRocePort = 4791;   // src/roce_enum.py ROCE_PORT
+constexpr uint32_t kAckValue = 31;     // CREDIT_CNT_INVALID, src/roce_enum.py:8
+constexpr uint32_t kPktSegBad = 0x20;  // RICRC_PKT_SEG_BAD
+
+__device__ __forceinline__ uint32_t wr_pkt_num(uint32_t len, uint32_t pmtu) {
+  // Util.compute_wr_pkt_num, src/roce_util.py:183-185
+  return len ? (uint32_t)(((uint64_t)len + pmtu - 1) / pmtu) : 1u;
+}
+
+// Everything a lane needs to produce its packet's frame dwords.
+struct Seg {
+  const uint8_t* src;  // payload start in the MR
+  uint8_t* dst;        // slot start
+  uint32_t plen;       // payload bytes
+  int hd;              // header dwords: IPv4 5 + UDP 2 + BTH 3 + extension headers
+  int T;               // frame dwords incl. the ICRC slot
+  int F;               // dwords fully defined without masking: hd + plen / 4
+  // header dwords (big-endian values) except the checksums
+  uint32_t h0, h3, h4, h5, h6, h7, h8, h9;
+  uint32_t e[5];       // extension header dwords
+  uint32_t ipcs;       // IPv4 header checksum
+  bool live;
+};
+
+__device__ __forceinline__ uint32_t fold16(uint32_t s) {
+  s = (s & 0xFFFFu) + (s >> 16);
+  s = (s & 0xFFFFu) + (s >> 16);
+  return s;
+}
+
+// The packet of index `pkt`: its WR, opcode, extension headers and geometry
+// (the rules of src/roce_sq.py:1243-1411 and src/roce_rq.py:388-438).
+__device__ __forceinline__ Seg describe_seg(const SegArgs& a, uint32_t pkt, bool inrange,
+                                            uint32_t& status) {
+  Seg s;
+  status = 0;
+  s.live = false;
+  s.src = a.mr;
+  s.dst = a.frames + (uint64_t)pkt * a.slot;
+  s.plen = 0;
+  s.hd = 10;
+  s.T = 0;
+  s.F = 0;
+  s.h0 = s.h3 = s.h4 = s.h5 = s.h6 = s.h7 = s.h8 = s.h9 = 0;
+  s.e[0] = s.e[1] = s.e[2] = s.e[3] = s.e[4] = 0;
+  s.ipcs = 0;
+  if (!inrange) return s;
+  const uint32_t w = a.lens[pkt];
+  status = kPktSegBad;
+  if (w >= a.nwr) return s;
+  const ricrc_seg_wr& wr = a.wrs[w];
+  const uint64_t mo = wr.mr_offset;
+  const uint32_t len = wr.length, op = wr.op;
+  const uint32_t n = wr_pkt_num(len, a.pmtu);
+  const uint32_t k = pkt - wr.first_pkt;
+  if (pkt < wr.first_pkt || k >= n || op > RICRC_SEG_READ_RESPONSE || mo > a.mr_bytes ||
+      len > a.mr_bytes - mo)
+    return s;
+  status = 0;
+  s.live = true;
+  const bool last = k == n - 1, first = k == 0;
+  const bool sig = (wr.flags & RICRC_SEG_SIGNALED) != 0;
+  const bool sol = (wr.flags & RICRC_SEG_SOLICITED) != 0;
+  // payload: full PMTU slices, the remainder on the last packet (none if len == 0)
+  const uint32_t off = k * a.pmtu;
+  s.plen = last ? len - off : a.pmtu;
+  s.src = a.mr + mo + off;
+
+  uint32_t opc, ext = 0;  // ext: 0 none, 1 one dword (ImmDt/IETH/AETH), 4 RETH, 5 RETHImmDt
+  uint32_t e0 = 0;
+  bool ack = false, se = false;
+  const uint32_t va_hi = (uint32_t)(wr.remote_va >> 32), va_lo = (uint32_t)wr.remote_va;
+  if (op <= RICRC_SEG_SEND_WITH_INV) {
+    if (!last) {
+      opc = first ? 0x00u : 0x01u;  // SEND_FIRST / SEND_MIDDLE
+    } else {
+      const bool only = n == 1;
+      opc = op == RICRC_SEG_SEND ? (only ? 0x04u : 0x02u)
+            : op == RICRC_SEG_SEND_WITH_IMM ? (only ? 0x05u : 0x03u)
+                                            : (only ? 0x17u : 0x16u);
+      if (op != RICRC_SEG_SEND) {
+        ext = 1;
+        e0 = wr.imm;  // ImmDt.data / IETH.rkey
+      }
+      ack = sig;
+      se = sol;
+    }
+  } else if (op <= RICRC_SEG_RDMA_WRITE_WITH_IMM) {
+    const bool imm = op == RICRC_SEG_RDMA_WRITE_WITH_IMM;
+    if (!last) {
+      opc = first ? 0x06u : 0x07u;  // RDMA_WRITE_FIRST (+RETH) / MIDDLE
+      ext = first ? 4 : 0;
+    } else if (n == 1) {
+      opc = imm ? 0x0Bu : 0x0Au;  // RDMA_WRITE_ONLY[_WITH_IMMEDIATE]: RETH[ImmDt]
+      ext = imm ? 5 : 4;
+    } else {
+      opc = imm ? 0x09u : 0x08u;  // RDMA_WRITE_LAST[_WITH_IMMEDIATE]: [ImmDt]
+      ext = imm ? 1 : 0;
+      e0 = wr.imm;
+    }
+    if (last) {
+      ack = sig;
+      se = imm && sol;
+    }
+  } else {  // RDMA READ response: AETH on FIRST / LAST / ONLY
+    opc = n == 1 ? 0x10u : first ? 0x0Du : last ? 0x0Fu : 0x0Eu;
+    if (first || last) {
+      ext = 1;
+      e0 = (kAckValue << 24) | (wr.msn & 0xFFFFFFu);  // rsvd 0, code ACK 0, value 31, msn
+    }
+  }
+  if (ext >= 4) {
+    s.e[0] = va_hi;
+    s.e[1] = va_lo;
+    s.e[2] = wr.rkey;
+    s.e[3] = len;  // RETH.dlen = message length
+    s.e[4] = wr.imm;
+  } else {
+    s.e[0] = e0;
+  }
+  s.hd = 10 + (int)ext;
+  const uint32_t pad = (4u - (s.plen & 3u)) & 3u;
+  const int pdw = (int)((s.plen + 3u) >> 2);
+  s.T = s.hd + pdw + 1;
+  s.F = s.hd + (int)(s.plen >> 2);
+  const uint32_t tl = 4u * (uint32_t)s.T;
+  s.h0 = 0x45000000u | tl;
+  s.h3 = wr.src_ip;
+  s.h4 = wr.dst_ip;
+  s.h5 = ((uint32_t)wr.sport << 16) | kRocePort;
+  s.h6 = (tl - 20u) << 16;  // UDP length, checksum filled in at the end
+  s.h7 = (opc << 24) | ((se ? 0x80u : 0u) << 16) | (pad << 20) | 0xFFFFu;  // SE|M|PadCnt|TVer, P_Key
+  s.h8 = wr.dqpn & 0xFFFFFFu;                                              // FECN|BECN|resv6 = 0
+  s.h9 = (ack ? 0x80000000u : 0u) | ((wr.psn + k) & 0xFFFFFFu);
+  // IPv4 header checksum over 0x4500, tl, id 1, frag 0, ttl 64 | proto 17, src, dst
+  const uint32_t sum = 0x4500u + tl + 1u + 0x4011u + (s.h3 >> 16) + (s.h3 & 0xFFFFu) +
+                       (s.h4 >> 16) + (s.h4 & 0xFFFFu);
+  s.ipcs = (~fold16(sum)) & 0xFFFFu;
+  return s;
+}
+
+// Header dword 4c + t (< hd) in memory (little-endian) order; t is a
+// compile-time constant and c the lane's chunk (0..3), so this is three
+// selects (a switch on the dword index becomes a private-memory table).
+template <int t>
+__device__ __forceinline__ uint32_t header_dword(const Seg& s, int c) {
+  constexpr uint32_t kId = 0x00010000u;  // id 1, flags/frag 0
+  uint32_t v0, v1, v2, v3;
+  if constexpr (t == 0) {
+    v0 = s.h0; v1 = s.h4; v2 = s.h8; v3 = s.e[2];
+  } else if constexpr (t == 1) {
+    v0 = kId; v1 = s.h5; v2 = s.h9; v3 = s.e[3];
+  } else if constexpr (t == 2) {
+    v0 = 0x40110000u | s.ipcs; v1 = s.h6; v2 = s.e[0]; v3 = s.e[4];  // ttl 64, proto 17
+  } else {
+    v0 = s.h3; v1 = s.h7; v2 = s.e[1]; v3 = 0u;
+  }
+  const uint32_t v = c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3;
+  return __builtin_bswap32(v);
+}
+
+// 16 payload bytes from `p`; bytes at or past `end` (the MR end) are not read.
+__device__ __forceinline__ u32x4 load_payload(const uint8_t* p, const uint8_t* end) {
+  if (p + 16 <= end) return __builtin_nontemporal_load((const u32x4_u*)p);
+  uint64_t lo = 0, hi = 0;  // (rare: the last chunk of a message that ends the MR)
+  for (int b = 0; b < 16 && p + b < end; ++b) {
+    const uint64_t v = p[b];
+    if (b < 8)
+      lo |= v << (8 * b);
+    else
+      hi |= v << (8 * (b - 8));
+  }
+  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// Keep the low `valid` bytes of a payload dword (valid <= 0: none).
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t v, int valid) {
+  return valid >= 4 ? v : valid <= 0 ? 0u : (v & ((1u << (8 * valid)) - 1u));
+}
+
+// A chunk outside the body: header dwords (HEAD only: all of them lie in the
+// first ceil(hd / DPI) iterations), payload with its zero pad, the (zero)
+// ICRC slot and zeros past the frame end.
+template <bool HEAD>
+__device__ __forceinline__ u32x4 edge_chunk(const Seg& s, int idx0, const uint8_t* mr_end) {
+  const int mbase = idx0 > s.hd ? idx0 - s.hd : 0;  // first payload dword of the chunk
+  u32x4 v = {0, 0, 0, 0};
+  if (s.live && 4 * mbase < (int)s.plen && idx0 + 3 >= s.hd) v = load_payload(s.src + 4 * mbase, mr_end);
+  u32x4 w;
+#define RICRC_EDGE(c, t)                                                                  \
+  {                                                                                       \
+    const int idx = idx0 + (t);                                                           \
+    const int m = idx - s.hd;                                                             \
+    const uint32_t pay = keep_bytes(pick4(v, m - mbase, 0u), (int)s.plen - 4 * m);       \
+    if constexpr (HEAD)                                                                   \
+      w.c = idx < s.hd ? header_dword<(t)>(s, idx0 >> 2) : pay;                           \
+    else                                                                                  \
+      w.c = pay;                                                                          \
+  }
+  RICRC_EDGE(x, 0)
+  RICRC_EDGE(y, 1)
+  RICRC_EDGE(z, 2)
+  RICRC_EDGE(w, 3)
+#undef RICRC_EDGE
+  return w;
+}
+
+// One's-complement accumulation of UDP bytes (dwords >= 5) in memory order.
+__device__ __forceinline__ void csum_add(uint64_t& acc, const u32x4& w) {
+  acc += (uint64_t)w.x + w.y + w.z + w.w;
+}
+
+template <int LOG2G>
+__global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
+  constexpr int PPW = 64 / G;
+  constexpr int U = kSegUnroll;
+  const int tid = threadIdx.x;
+  stage_tables<LOG2G>(a.tables, tid);
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int gl = lane & (G - 1);
+  const int grp = lane >> LOG2G;
+  const int base = grp * G;
+  const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
+  const uint32_t kc1 = kc0 | 0x10000u;
+  const uint8_t* mr_end = a.mr + a.mr_bytes;
+  const uint32_t nsets = (a.npkts + PPW - 1) / PPW;
+  const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
+  const uint32_t set_begin = blockIdx.x * per_block;
+  const uint32_t set_end = min(nsets, set_begin + per_block);
+
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
+    const uint32_t pkt = set * PPW + grp;
+    uint32_t status;
+    const Seg s = describe_seg(a, pkt, pkt < a.npkts, status);
+    // CRC geometry (frame at grid column 0): n covered dwords, J iterations,
+    // r valid columns in the last one
+    const int n = s.live ? s.T - 1 : 1;
+    const int J = (n + DPI - 1) / DPI;
+    const int r = n - DPI * (J - 1);
+    const int Jw = s.live ? (s.T + DPI - 1) / DPI : 0;  // iterations that write
+    const int jh = min((s.hd + DPI - 1) / DPI, Jw);     // head iterations
+    const int jb = max(jh, min(s.F / DPI, Jw));         // body: [jh, jb)
+    const int t_last = s.T - 1;                          // ICRC slot dword
+
+    Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    uint64_t acc = 0;
+    u32x4 keep6 = {0, 0, 0, 0}, keepT = {0, 0, 0, 0};
+    bool has6 = false, hasT = false;
+
+    auto edge = [&](int j, auto head) {
+      const int idx0 = DPI * j + 4 * gl;
+      if (idx0 >= s.T) return;
+      u32x4 w = edge_chunk<decltype(head)::value>(s, idx0, mr_end);
+      // UDP one's-complement sum: dwords 5 .. T-2 (the ICRC slot is still zero)
+      u32x4 cs = w;
+      if (idx0 + 0 < 5) cs.x = 0;
+      if (idx0 + 1 < 5) cs.y = 0;
+      if (idx0 + 2 < 5) cs.z = 0;
+      if (idx0 + 3 < 5) cs.w = 0;
+      csum_add(acc, cs);
+      const bool h6 = idx0 <= 6 && 6 < idx0 + 4;
+      const bool hT = idx0 <= t_last && t_last < idx0 + 4;
+      if (h6) {
+        keep6 = w;
+        has6 = true;
+      }
+      if (hT) {
+        keepT = w;
+        hasT = true;
+      }
+      if (!h6 && !hT) __builtin_nontemporal_store(w, (u32x4*)(s.dst + 4 * idx0));
+      if (j < J) {  // CRC: masked header dwords, seed, columns past the end skipped
+        w.x = fix_dword(w.x, idx0 + 0, 6, 8);
+        w.y = fix_dword(w.y, idx0 + 1, 6, 8);
+        w.z = fix_dword(w.z, idx0 + 2, 6, 8);
+        w.w = fix_dword(w.w, idx0 + 3, 6, 8);
+        if (j == J - 1)
+          fold_last(A, w, idx0, n, kc0, kc1);
+        else
+          fold(A, w, kc0, kc1);
+      }
+    };
+
+    for (int j = 0; j < jh; ++j) edge(j, std::true_type{});
+    // body: every dword is payload, full and covered by the CRC; MR loads run
+    // one block of U iterations ahead of the stores and folds
+    {
+      const uint8_t* src = s.src + 4 * (4 * gl - s.hd);
+      uint8_t* dst = s.dst + 16 * gl;
+      u32x4 cur[U], nxt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (jh + u < jb) cur[u] = __builtin_nontemporal_load((const u32x4_u*)(src + 4 * DPI * (jh + u)));
+      for (int j0 = jh; j0 < jb; j0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (j0 + U + u < jb)
+            nxt[u] = __builtin_nontemporal_load((const u32x4_u*)(src + 4 * DPI * (j0 + U + u)));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (j0 + u < jb) {
+            __builtin_nontemporal_store(cur[u], (u32x4*)(dst + 4 * DPI * (j0 + u)));
+            csum_add(acc, cur[u]);
+            fold(A, cur[u], kc0, kc1);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+      }
+    }
+    for (int j = jb; j < Jw; ++j) edge(j, std::false_type{});
+
+    // ---- group combine: ICRC, then the UDP checksum over the final bytes -----
+    const uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                      A.P[3] ^ A.T[3], r, gl, base);
+    const uint32_t icrc = ~B;
+    uint32_t f = (uint32_t)acc;
+    f = (f & 0xFFFFu) + (f >> 16) + (uint32_t)(acc >> 32);
+#pragma unroll
+    for (int l = 0; l < LOG2G; ++l) f += (uint32_t)__shfl_xor((int)f, 1 << l, 64);
+    if (s.live) {
+      // pseudo header (src, dst, proto 17, UDP length) in memory byte order,
+      // plus the ICRC; the UDP header and payload are in f
+      const uint32_t ulen = 4u * (uint32_t)s.T - 20u;
+      uint32_t t = f + __builtin_bswap16((uint16_t)(s.h3 >> 16)) + __builtin_bswap16((uint16_t)s.h3) +
+                   __builtin_bswap16((uint16_t)(s.h4 >> 16)) + __builtin_bswap16((uint16_t)s.h4) +
+                   0x1100u + __builtin_bswap16((uint16_t)ulen) + (icrc & 0xFFFFu) + (icrc >> 16);
+      t = fold16(fold16(t));
+      uint32_t c = (~t) & 0xFFFFu;
+      if (c == 0) c = 0xFFFFu;  // UDP: a computed 0 goes out as 0xFFFF
+      if (has6) {
+        keep6.z = (keep6.z & 0xFFFFu) | (c << 16);
+        __builtin_nontemporal_store(keep6, (u32x4*)(s.dst + 16));
+      }
+      if (hasT) {
+        const int tt = t_last & 3;
+        keepT.x = tt == 0 ? icrc : keepT.x;
+        keepT.y = tt == 1 ? icrc : keepT.y;
+        keepT.z = tt == 2 ? icrc : keepT.z;
+        keepT.w = tt == 3 ? icrc : keepT.w;
+        __builtin_nontemporal_store(keepT, (u32x4*)(s.dst + 4 * (t_last & ~3)));
+      }
+    }
+    if (pkt < a.npkts && gl == 0) {
+      a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;
+      if (a.icrc_out) a.icrc_out[pkt] = s.live ? icrc : 0u;
+      if (a.status_out) a.status_out[pkt] = (uint8_t)status;
+    }
+  }
+}
+
+// Packet -> WR map: lens[first_pkt + k] = WR index, one workgroup per WR.
+__global__ void __launch_bounds__(256) seg_map_kernel(SegArgs a) {
+  for (uint32_t w = blockIdx.x; w < a.nwr; w += gridDim.x) {
+    const uint32_t fp = a.wrs[w].first_pkt;
+    const uint32_t cnt = wr_pkt_num(a.wrs[w].length, a.pmtu);
+    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+      const uint64_t p = (uint64_t)fp + k;
+      if (p < a.npkts) a.lens[p] = w;
+    }
+  }
+}
+
+// STREAM-style copy with the segmentation kernel's geometry: one 1024-thread
+// workgroup per CU over a contiguous chunk, 16-byte nt loads and stores.
+__global__ void __launch_bounds__(1024) stream_copy_kernel(const u32x4* __restrict__ src,
+                                                           u32x4* __restrict__ dst, uint64_t n16) {
+  constexpr int R = 4;
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per;
+  const uint64_t b1 = b0 + per < n16 ? b0 + per : n16;
+  uint64_t i = b0 + threadIdx.x;
+  for (; i + (R - 1) * 1024 < b1; i += R * 1024) {
+    u32x4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load(src + i + r * 1024);
+#pragma unroll
+    for (int r = 0; r < R; ++r) __builtin_nontemporal_store(v[r], dst + i + r * 1024);
+  }
+  for (; i < b1; i += 1024) dst[i] = src[i];
+}
+
+typedef void (*seg_fn)(SegArgs);
+
+seg_fn select_segment(int log2g) {
+  switch (log2g) {
+    case 1: return segment_kernel<1>;
+    case 2: return segment_kernel<2>;
+    case 3: return segment_kernel<3>;
+    case 4: return segment_kernel<4>;
+    default: return nullptr;
+  }
+}
+
+size_t seg_lds_bytes(int log2g) { return kLdsMain + 4096u * (1 + log2g) + 256u; }
+
+}  // namespace
+
+hipError_t launch_segment(const SegArgs& a, int log2g, int num_cus, hipStream_t stream) {
+  if (a.npkts == 0) return hipSuccess;
+  seg_fn k = select_segment(log2g);
+  if (!k) return hipErrorInvalidValue;
+  static bool prepared[5] = {false, false, false, false, false};
+  if (!prepared[log2g]) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)seg_lds_bytes(log2g));
+    if (e != hipSuccess) return e;
+    prepared[log2g] = true;
+  }
+  if (a.nwr) {
+    const uint32_t mb = a.nwr < 8192u ? a.nwr : 8192u;
+    hipLaunchKernelGGL(seg_map_kernel, dim3(mb), dim3(256), 0, stream, a);
+  }
+  const uint32_t ppw = 64u >> log2g;
+  const uint64_t nsets = (a.npkts + ppw - 1) / ppw;
+  uint64_t blocks = (nsets + 15) / 16;
+  if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), seg_lds_bytes(log2g), stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_copy(const uint8_t* src, uint8_t* dst, uint64_t bytes, int num_cus,
+                              hipStream_t stream) {
+  const uint64_t n16 = bytes / 16;
+  if (n16 == 0) return hipSuccess;
+  hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)num_cus), dim3(1024), 0, stream,
+                     (const u32x4*)src, (u32x4*)dst, n16);
+  return hipGetLastError();
+}
+
+}  // namespace ricrc

@@ -15,4 +15,6 @@ from .engine import (  # noqa: F401
     compute_batch_multi,
     load_library,
     pack_icrc,
+    seg_wrs,
+    segment_plan,
 )

@@ -30,6 +30,22 @@ PKT_NOT_UDP = 0x04
 PKT_LEN_MISMATCH = 0x08
 PKT_ICRC_MISMATCH = 0x10
 PKT_FATAL = PKT_BAD_LEN | PKT_NOT_IPV4 | PKT_NOT_UDP
+PKT_SEG_BAD = 0x20
+
+# segmentation work-request ops and flags (RICRC_SEG_*)
+SEG_SEND, SEG_SEND_WITH_IMM, SEG_SEND_WITH_INV = 0, 1, 2
+SEG_RDMA_WRITE, SEG_RDMA_WRITE_WITH_IMM, SEG_READ_RESPONSE = 3, 4, 5
+SEG_SIGNALED, SEG_SOLICITED = 0x1, 0x2
+
+# struct ricrc_seg_wr (include/roce_icrc.h), 64 bytes, as a numpy record so
+# large WR batches are built vectorised
+SEG_WR_DTYPE = np.dtype([
+    ("mr_offset", "<u8"), ("remote_va", "<u8"), ("length", "<u4"), ("psn", "<u4"),
+    ("dqpn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("rkey", "<u4"), ("imm", "<u4"),
+    ("msn", "<u4"), ("sport", "<u2"), ("op", "u1"), ("flags", "u1"), ("first_pkt", "<u4"),
+    ("reserved", "<u4", (2,)),
+])
+assert SEG_WR_DTYPE.itemsize == 64
 
 
 class IcrcUnavailable(RuntimeError):
@@ -93,6 +109,18 @@ _SIGNATURES = {
     ),
     "ricrc_stream_read_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "ricrc_lanes_for_len": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "ricrc_segment_plan": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    "ricrc_segment": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, ctypes.c_size_t,
+         _vp, _vp, _vp],
+    ),
+    "ricrc_segment_dev": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _vp,
+         ctypes.c_uint32, _vp, _vp, _vp, _vp],
+    ),
+    "ricrc_stream_copy_dev": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp]),
 }
 
 _lib = None
@@ -283,9 +311,55 @@ class IcrcEngine:
             self.ctx, _ptr(d_frames), _ptr(d_offsets), _ptr(d_lens), n, _ptr(d_ok), _ptr(d_icrc),
             _ptr(d_status), stream))
 
+    # -- MR -> packet segmentation fused with the ICRC ------------------------
+    def segment(self, mr, wrs: np.ndarray, pmtu: int):
+        """Build every frame of a WR batch on the GPU (process_send_req /
+        process_write_req / ReadReqCtx.commit, src/roce_sq.py:1243-1411,
+        src/roce_rq.py:388-438).  Plans ``wrs`` in place.  Returns
+        (frames [npkts, slot] uint8, lens, icrc, status)."""
+        m = _u8(mr)
+        npkts, slot = segment_plan(wrs, pmtu)
+        frames = np.zeros((npkts, slot), np.uint8)
+        lens = np.zeros(npkts, np.uint32)
+        icrc = np.zeros(npkts, np.uint32)
+        st = np.zeros(npkts, np.uint8)
+        self._check("ricrc_segment", self.lib.ricrc_segment(
+            self.ctx, _ptr(m), m.size, _ptr(wrs), wrs.size, pmtu, _ptr(frames), frames.size,
+            _ptr(lens), _ptr(icrc), _ptr(st)))
+        return frames, lens, icrc, st
+
+    def segment_dev(self, d_mr, mr_bytes, d_wrs, nwr, pmtu, npkts, d_frames, slot, d_lens,
+                    d_icrc=None, d_status=None, stream=None):
+        self._check("ricrc_segment_dev", self.lib.ricrc_segment_dev(
+            self.ctx, _ptr(d_mr), mr_bytes, _ptr(d_wrs), nwr, pmtu, npkts, _ptr(d_frames), slot,
+            _ptr(d_lens), _ptr(d_icrc), _ptr(d_status), stream))
+
+    def stream_copy_dev(self, d_src, d_dst, nbytes, stream=None):
+        self._check("ricrc_stream_copy_dev", self.lib.ricrc_stream_copy_dev(
+            self.ctx, _ptr(d_src), _ptr(d_dst), nbytes, stream))
+
     def stream_read_dev(self, d_buf, nbytes, d_sink, stream=None):
         self._check("ricrc_stream_read_dev", self.lib.ricrc_stream_read_dev(
             self.ctx, _ptr(d_buf), nbytes, _ptr(d_sink), stream))
+
+
+def seg_wrs(n: int) -> np.ndarray:
+    """A zeroed array of n ``ricrc_seg_wr`` records."""
+    return np.zeros(n, dtype=SEG_WR_DTYPE)
+
+
+def segment_plan(wrs: np.ndarray, pmtu: int) -> tuple[int, int]:
+    """Util.compute_wr_pkt_num over a WR batch (host only, no GPU): fills
+    ``wrs['first_pkt']`` in place, returns (total packets, slot bytes)."""
+    if wrs.dtype != SEG_WR_DTYPE or not wrs.flags.c_contiguous:
+        raise ValueError("wrs must be a C-contiguous SEG_WR_DTYPE array")
+    lib = load_library()
+    n = ctypes.c_uint32(0)
+    slot = ctypes.c_uint32(0)
+    rc = lib.ricrc_segment_plan(_ptr(wrs), wrs.size, pmtu, ctypes.byref(n), ctypes.byref(slot))
+    if rc != RICRC_OK:
+        raise IcrcError("ricrc_segment_plan", rc, lib.ricrc_strerror(rc).decode())
+    return n.value, slot.value
 
 
 def compute_batch_multi(engines: list[IcrcEngine], frames, offsets, lens):

@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_errors():
     lib = E.load_library()
-    assert lib.ricrc_abi_version() == 1
+    assert lib.ricrc_abi_version() == 2
     assert lib.ricrc_strerror(0) == b"ok"
     assert lib.ricrc_strerror(-22) == b"invalid argument"
     assert lib.ricrc_strerror(-19) == b"no usable gfx950 device"
