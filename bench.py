@@ -14,7 +14,7 @@ Printed (rank 0): ONE JSON line with the driver's keys plus
   roofline      -- achieved algorithmic GB/s of the ICRC kernel (per-launch
                    bytes / mean launch time from HIP events on the launch
                    stream) against the 8.0 TB/s HBM peak, and the PMC-measured
-                   HBM traffic per launch when profiles/pmc_traffic.json holds
+                   HBM traffic per launch when profiles/pmc_traffic_<workload>.json holds
                    it for this workload;
   cpu_baseline  -- the per-packet Python restatement of BTH.compute_icrc
                    (datenlord/roce-sim src/roce.py:192-223, zlib.crc32), timed
@@ -36,7 +36,7 @@ sys.path.insert(0, str(ROOT / "roce-sim_amd"))
 
 METRIC = "ICRC GiB/s device-resident, 4 KiB MTU packets, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
+PMC_DIR = ROOT / "profiles"  # pmc_traffic_<workload>.json (scripts/pmc_traffic.py)
 
 WORKLOADS = {
     # name: (payload bytes (0 = mixed MTU), packets per GPU, seed, description)
@@ -254,15 +254,24 @@ def cpu_baseline_seg(mr: np.ndarray, rec: np.ndarray, pmtu: int, frames_ok):
     except AttributeError:
         cores = os.cpu_count() or 1
     procs = max(1, min(16, cores))
-    nw = min(rec.size, 16 * procs)  # 64 packets per WR: ~1k packets per process
-    wrs = [so.SegWR(op=int(r["op"]), mr_offset=int(r["mr_offset"]), length=int(r["length"]),
+    mv = memoryview(mr)
+
+    def sample(nw):
+        return [so.SegWR(op=int(r["op"]), mr_offset=int(r["mr_offset"]), length=int(r["length"]),
                     psn=int(r["psn"]), dqpn=int(r["dqpn"]), src_ip=int(r["src_ip"]),
                     dst_ip=int(r["dst_ip"]), sport=int(r["sport"]), flags=int(r["flags"]),
                     imm=int(r["imm"])) for r in rec[:nw]]
-    mv = memoryview(mr)
+
+    # calibrate on one WR, then size the sample for about 10 s of pool time
+    t0 = time.perf_counter()
+    so.segment(mv, sample(1), pmtu)
+    t1 = time.perf_counter() - t0
+    nw = int(min(rec.size, max(procs, 10.0 * procs / max(t1, 1e-6))))
+    wrs = sample(nw)
     global _CPU_JOB
     _CPU_JOB = (mv, wrs, pmtu)
-    chunks = [(i, i + 1) for i in range(nw)]
+    step = max(1, nw // (4 * procs))
+    chunks = [(i, min(nw, i + step)) for i in range(0, nw, step)]
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(procs) as pool:
         cov = sum(pool.map(_cpu_seg_chunk, chunks))
@@ -342,6 +351,8 @@ class Segment:
         return "stream_copy_GBps", 2 * nb / float(np.median(ts)) / 1e9
 
     def frames_ok(self):
+        self.step(self.torch.cuda.current_stream().cuda_stream)  # ceiling() reused the buffer
+        self.torch.cuda.synchronize()
         fr = self.d_frames[: 64 * self.slot].cpu().numpy().reshape(64, self.slot)
         lens = self.d_lens[:64].cpu().numpy()
         return lambda p, f: lens[p] == len(f) and fr[p, : len(f)].tobytes() == f
@@ -460,9 +471,10 @@ def main():
         mean_k = float(np.mean(kern_s))
         achieved = W.alg_bytes / mean_k / 1e9
         traffic = None
-        if PMC_FILE.exists():
+        pmc_file = PMC_DIR / f"pmc_traffic_{args.workload}.json"
+        if pmc_file.exists():
             try:
-                pmc = json.loads(PMC_FILE.read_text())
+                pmc = json.loads(pmc_file.read_text())
                 if pmc.get("workload") == args.workload and pmc.get("packets") == n:
                     traffic = pmc.get("traffic_bytes_per_launch")
             except (ValueError, OSError):

@@ -38,6 +38,15 @@ namespace {
 
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
+// 16-byte MR read (any alignment).
+__device__ __forceinline__ u32x4 ldmr(const uint8_t* p) {
+#ifdef RICRC_SEG_NT_LOADS
+  return __builtin_nontemporal_load((const u32x4_u*)p);
+#else
+  return *(const u32x4_u*)p;
+#endif
+}
+
 constexpr int kSegUnroll = 4;          // body iterations (16-byte MR loads per lane) in flight
 constexpr uint32_t kRocePort = 4791;   // src/roce_enum.py ROCE_PORT
 constexpr uint32_t kAckValue = 31;     // CREDIT_CNT_INVALID, src/roce_enum.py:8
@@ -200,18 +209,23 @@ __device__ __forceinline__ uint32_t header_dword(const Seg& s, int c) {
   return __builtin_bswap32(v);
 }
 
-// 16 payload bytes from `p`; bytes at or past `end` (the MR end) are not read.
-__device__ __forceinline__ u32x4 load_payload(const uint8_t* p, const uint8_t* end) {
-  if (p + 16 <= end) return __builtin_nontemporal_load((const u32x4_u*)p);
-  uint64_t lo = 0, hi = 0;  // (rare: the last chunk of a message that ends the MR)
-  for (int b = 0; b < 16 && p + b < end; ++b) {
-    const uint64_t v = p[b];
-    if (b < 8)
-      lo |= v << (8 * b);
-    else
-      hi |= v << (8 * (b - 8));
-  }
-  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+// 16 payload bytes from `p` without reading past `hi + 16` (hi = the MR end
+// minus 16): one unconditional load at min(p, hi), then a byte shift in
+// registers.  Bytes that would lie past the MR end come out as garbage; they
+// are past the message, so the caller masks them.  Only waves that can reach
+// the MR end use this form (see segment_kernel).
+__device__ __forceinline__ u32x4 load_payload_clamped(const uint8_t* p, const uint8_t* hi) {
+  const uint8_t* q = p < hi ? p : hi;
+  const u32x4 v = ldmr(q);
+  const uint32_t d = (uint32_t)(p - q);
+  const int k = (int)(d >> 2);
+  const uint32_t sh = d & 3u;
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(pick4(v, k + 1, 0u), pick4(v, k, 0u), sh);
+  o.y = __builtin_amdgcn_alignbyte(pick4(v, k + 2, 0u), pick4(v, k + 1, 0u), sh);
+  o.z = __builtin_amdgcn_alignbyte(pick4(v, k + 3, 0u), pick4(v, k + 2, 0u), sh);
+  o.w = __builtin_amdgcn_alignbyte(pick4(v, k + 4, 0u), pick4(v, k + 3, 0u), sh);
+  return o;
 }
 
 // Keep the low `valid` bytes of a payload dword (valid <= 0: none).
@@ -219,14 +233,13 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t v, int valid) {
   return valid >= 4 ? v : valid <= 0 ? 0u : (v & ((1u << (8 * valid)) - 1u));
 }
 
-// A chunk outside the body: header dwords (HEAD only: all of them lie in the
-// first ceil(hd / DPI) iterations), payload with its zero pad, the (zero)
-// ICRC slot and zeros past the frame end.
+// A chunk outside the full-payload body: header dwords (HEAD only: all of
+// them lie in the first block), payload with its zero pad, the (zero) ICRC
+// slot and zeros past the frame end.  `v` holds the 16 MR bytes at payload
+// dword max(idx0 - hd, 0) (see seg_load).
 template <bool HEAD>
-__device__ __forceinline__ u32x4 edge_chunk(const Seg& s, int idx0, const uint8_t* mr_end) {
-  const int mbase = idx0 > s.hd ? idx0 - s.hd : 0;  // first payload dword of the chunk
-  u32x4 v = {0, 0, 0, 0};
-  if (s.live && 4 * mbase < (int)s.plen && idx0 + 3 >= s.hd) v = load_payload(s.src + 4 * mbase, mr_end);
+__device__ __forceinline__ u32x4 edge_chunk(const Seg& s, int idx0, const u32x4& v) {
+  const int mbase = idx0 > s.hd ? idx0 - s.hd : 0;
   u32x4 w;
 #define RICRC_EDGE(c, t)                                                                  \
   {                                                                                       \
@@ -268,6 +281,9 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
   const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
   const uint32_t kc1 = kc0 | 0x10000u;
   const uint8_t* mr_end = a.mr + a.mr_bytes;
+  // lowest start of a 16-byte read that stays inside the MR (an MR shorter
+  // than 16 bytes must be readable for 16, include/roce_icrc.h)
+  const uint8_t* mr_hi = a.mr_bytes >= 16 ? mr_end - 16 : a.mr;
   const uint32_t nsets = (a.npkts + PPW - 1) / PPW;
   const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
   const uint32_t set_begin = blockIdx.x * per_block;
@@ -283,19 +299,29 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
     const int J = (n + DPI - 1) / DPI;
     const int r = n - DPI * (J - 1);
     const int Jw = s.live ? (s.T + DPI - 1) / DPI : 0;  // iterations that write
-    const int jh = min((s.hd + DPI - 1) / DPI, Jw);     // head iterations
-    const int jb = max(jh, min(s.F / DPI, Jw));         // body: [jh, jb)
+    const int nblk = (Jw + U - 1) / U;                  // blocks of U iterations
     const int t_last = s.T - 1;                          // ICRC slot dword
+
+    // Every MR load is unconditional, so the compiler can count the loads in
+    // flight (a predicated load forces a full vmcnt(0) drain).  Iteration j
+    // of a block >= 1 reads the 16 payload bytes at dword DPI j + 4 gl - hd
+    // from one base pointer (immediate offsets); block 0 clamps header lanes
+    // to dword 0.  Reads run up to one block past the frame (into the next
+    // packet's bytes); a wave that could read past the MR end takes the
+    // clamped-and-shifted form of every load instead.
+    const int far = max(DPI * (max(nblk, 2) * U - 1) + 4 * gl - s.hd, 0);
+    const bool guard = s.src + 4 * far + 16 > mr_end;
 
     Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     uint64_t acc = 0;
-    u32x4 keep6 = {0, 0, 0, 0}, keepT = {0, 0, 0, 0};
-    bool has6 = false, hasT = false;
 
-    auto edge = [&](int j, auto head) {
+    // Chunks holding the UDP checksum (dword 6) or the ICRC slot are stored
+    // with zeros there; the same lane rewrites those bytes once the group has
+    // combined (a lane's stores to one address stay in program order).
+    auto edge = [&](int j, const u32x4& v, auto head) {
       const int idx0 = DPI * j + 4 * gl;
       if (idx0 >= s.T) return;
-      u32x4 w = edge_chunk<decltype(head)::value>(s, idx0, mr_end);
+      u32x4 w = edge_chunk<decltype(head)::value>(s, idx0, v);
       // UDP one's-complement sum: dwords 5 .. T-2 (the ICRC slot is still zero)
       u32x4 cs = w;
       if (idx0 + 0 < 5) cs.x = 0;
@@ -303,17 +329,7 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
       if (idx0 + 2 < 5) cs.z = 0;
       if (idx0 + 3 < 5) cs.w = 0;
       csum_add(acc, cs);
-      const bool h6 = idx0 <= 6 && 6 < idx0 + 4;
-      const bool hT = idx0 <= t_last && t_last < idx0 + 4;
-      if (h6) {
-        keep6 = w;
-        has6 = true;
-      }
-      if (hT) {
-        keepT = w;
-        hasT = true;
-      }
-      if (!h6 && !hT) __builtin_nontemporal_store(w, (u32x4*)(s.dst + 4 * idx0));
+      __builtin_nontemporal_store(w, (u32x4*)(s.dst + 4 * idx0));
       if (j < J) {  // CRC: masked header dwords, seed, columns past the end skipped
         w.x = fix_dword(w.x, idx0 + 0, 6, 8);
         w.y = fix_dword(w.y, idx0 + 1, 6, 8);
@@ -325,35 +341,76 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
           fold(A, w, kc0, kc1);
       }
     };
-
-    for (int j = 0; j < jh; ++j) edge(j, std::true_type{});
-    // body: every dword is payload, full and covered by the CRC; MR loads run
-    // one block of U iterations ahead of the stores and folds
-    {
-      const uint8_t* src = s.src + 4 * (4 * gl - s.hd);
-      uint8_t* dst = s.dst + 16 * gl;
-      u32x4 cur[U], nxt[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (jh + u < jb) cur[u] = __builtin_nontemporal_load((const u32x4_u*)(src + 4 * DPI * (jh + u)));
-      for (int j0 = jh; j0 < jb; j0 += U) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (j0 + U + u < jb)
-            nxt[u] = __builtin_nontemporal_load((const u32x4_u*)(src + 4 * DPI * (j0 + U + u)));
+    // block b >= 1: the full-payload fast path when all its iterations lie in
+    // [hd, F) (no header, no mask, no ICRC slot), else the generic path
+    auto block = [&](int b, const u32x4* v) {
+      const int j0 = b * U;
+      if (DPI * (j0 + U) <= s.F) {
+        uint8_t* d = s.dst + 4 * (DPI * j0 + 4 * gl);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (j0 + u < jb) {
-            __builtin_nontemporal_store(cur[u], (u32x4*)(dst + 4 * DPI * (j0 + u)));
-            csum_add(acc, cur[u]);
-            fold(A, cur[u], kc0, kc1);
-          }
+          __builtin_nontemporal_store(v[u], (u32x4*)(d + 4 * DPI * u));
+          csum_add(acc, v[u]);
+          fold(A, v[u], kc0, kc1);
         }
+      } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < U; ++u) edge(j0 + u, v[u], std::false_type{});
       }
-    }
-    for (int j = jb; j < Jw; ++j) edge(j, std::false_type{});
+    };
+    // The block loop runs the wave's largest block count (a uniform trip
+    // count, so the two buffers ping-pong without waits on fresh loads); a
+    // group past its own last block re-reads that block (cache hits) and its
+    // chunks fall past the frame end.
+    int nbmax = nblk;
+#pragma unroll
+    for (int l = 1; l < 64; l <<= 1) nbmax = max(nbmax, __shfl_xor(nbmax, l, 64));
+    nbmax = __builtin_amdgcn_readfirstlane(nbmax);  // scalar: a uniform loop
+    auto run = [&](auto guarded) {
+      constexpr bool GUARD = decltype(guarded)::value;
+      // block b's loads, b clamped to [1, nblk - 1]
+      auto ld_block = [&](int b, u32x4* v) {
+        const int bc = max(min(b, nblk - 1), 1);
+        if constexpr (GUARD) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int m = max(DPI * min(bc * U + u, max(Jw - 1, 0)) + 4 * gl - s.hd, 0);
+            v[u] = load_payload_clamped(s.src + 4 * m, mr_hi);
+          }
+        } else {
+          // iterations past the packet's last one re-read that one (no HBM
+          // over-read into the next packet)
+          const uint8_t* p = s.src + 4 * (DPI * U * bc + 4 * gl - s.hd);
+          const int last = max(Jw - 1 - U * bc, 0);
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u] = ldmr(p + 4 * DPI * min(u, last));
+        }
+      };
+      u32x4 X[U], Y[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = max(DPI * u + 4 * gl - s.hd, 0);
+        if constexpr (GUARD)
+          Y[u] = load_payload_clamped(s.src + 4 * m, mr_hi);
+        else
+          Y[u] = ldmr(s.src + 4 * m);
+      }
+      ld_block(1, X);
+      // block 0 carries the header (hd <= 15 < DPI * U)
+#pragma unroll
+      for (int u = 0; u < U; ++u) edge(u, Y[u], std::true_type{});
+      for (int b = 1; b < nbmax; b += 2) {
+        ld_block(b + 1, Y);
+        block(b, X);
+        if (b + 1 >= nbmax) break;
+        ld_block(b + 2, X);
+        block(b + 1, Y);
+      }
+    };
+    if (__any(guard))
+      run(std::true_type{});
+    else
+      run(std::false_type{});
 
     // ---- group combine: ICRC, then the UDP checksum over the final bytes -----
     const uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
@@ -373,18 +430,11 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
       t = fold16(fold16(t));
       uint32_t c = (~t) & 0xFFFFu;
       if (c == 0) c = 0xFFFFu;  // UDP: a computed 0 goes out as 0xFFFF
-      if (has6) {
-        keep6.z = (keep6.z & 0xFFFFu) | (c << 16);
-        __builtin_nontemporal_store(keep6, (u32x4*)(s.dst + 16));
+      if (gl == (4 >> 2)) {  // the lane that stored dword 6 (iteration 0, G >= 2)
+        const uint16_t cs = (uint16_t)c;
+        *(uint16_t*)(s.dst + 26) = cs;
       }
-      if (hasT) {
-        const int tt = t_last & 3;
-        keepT.x = tt == 0 ? icrc : keepT.x;
-        keepT.y = tt == 1 ? icrc : keepT.y;
-        keepT.z = tt == 2 ? icrc : keepT.z;
-        keepT.w = tt == 3 ? icrc : keepT.w;
-        __builtin_nontemporal_store(keepT, (u32x4*)(s.dst + 4 * (t_last & ~3)));
-      }
+      if (gl == ((t_last & (DPI - 1)) >> 2)) *(uint32_t*)(s.dst + 4 * t_last) = icrc;
     }
     if (pkt < a.npkts && gl == 0) {
       a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;

@@ -26,10 +26,21 @@ echo "== pmc WRITE_SIZE"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcw_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmcw_$TAG.log 2>&1
 rc=$?; tail -2 $OUT/pmcw_$TAG.log; echo "pmcw rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R
-python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
-  --packets $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][1])") \
-  --frame-bytes $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][0] + 44)") \
-  --out $OUT/pmc_traffic_$TAG.json || exit 1
-python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json > $OUT/prof_summary_$TAG.txt || exit 1
+if [ "$WL" = seg ]; then
+  N=$(python3 -c "import bench; print(bench.WORKLOADS['seg'][1])")
+  MR=$((N * 4096))
+  python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload seg \
+    --packets $N --frame-bytes 4140 --kernel segment_kernel --ceiling stream_copy_kernel \
+    --ceiling-read-bytes $MR --alg-bytes $((MR + N * 4140 + 8 * N)) \
+    --out $OUT/pmc_traffic_${TAG}_seg.json || exit 1
+  KN=segment_kernel
+else
+  python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
+    --packets $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][1])") \
+    --frame-bytes $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][0] + 44)") \
+    --out $OUT/pmc_traffic_${TAG}_$WL.json || exit 1
+  KN=icrc_kernel
+fi
+python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json $KN > $OUT/prof_summary_$TAG.txt || exit 1
 cat $OUT/prof_summary_$TAG.txt
 exit 0

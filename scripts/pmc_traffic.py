@@ -8,7 +8,9 @@ loads), so the read side is calibrated on the STREAM-read kernel that
 bench.py runs over the SAME frame buffer (known byte count per launch).
 
 usage: python scripts/pmc_traffic.py --fetch DIR --write DIR --workload cfg2 \
-          --packets 1048576 --frame-bytes 4140 [--out profiles/pmc_traffic.json]
+          --packets 1048576 --frame-bytes 4140 [--out profiles/pmc_traffic_cfg2.json]
+       segmentation (seg): --kernel segment_kernel --ceiling stream_copy_kernel \
+          --ceiling-read-bytes <MR bytes> --alg-bytes <MR + frames + 8/packet>
 """
 import argparse
 import csv
@@ -48,36 +50,41 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--packets", type=int, required=True)
     ap.add_argument("--frame-bytes", type=int, required=True)
-    ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--kernel", default="icrc_kernel")
+    ap.add_argument("--ceiling", default="stream_read_kernel")
+    ap.add_argument("--ceiling-read-bytes", type=int, default=0)
+    ap.add_argument("--alg-bytes", type=int, default=0)
     a = ap.parse_args()
     fr = read_counters(a.fetch)
     wr = read_counters(a.write)
-    k_icrc = pick(fr, "icrc_kernel")
-    k_sr = pick(fr, "stream_read_kernel")
+    k_icrc = pick(fr, a.kernel)
+    k_sr = pick(fr, a.ceiling)
     n, flen = a.packets, a.frame_bytes
-    sr_bytes = (n * flen) // 16 * 16  # bench.py reads the whole frame buffer
+    # bench.py's ceiling kernel reads the whole frame buffer (ICRC) or the MR (seg)
+    sr_bytes = a.ceiling_read_bytes or (n * flen) // 16 * 16
     fetch_sr = mean(fr[k_sr]["FETCH_SIZE"]) * 1024
     calib = sr_bytes / fetch_sr
     fetch_icrc_raw = mean(fr[k_icrc]["FETCH_SIZE"]) * 1024
-    write_icrc = mean(wr[pick(wr, "icrc_kernel")]["WRITE_SIZE"]) * 1024
+    write_icrc = mean(wr[pick(wr, a.kernel)]["WRITE_SIZE"]) * 1024
     fetch_icrc = fetch_icrc_raw * calib
-    alg = n * flen  # C_i read + 4-B ICRC written = frame bytes per packet
+    alg = a.alg_bytes or n * flen  # ICRC: C_i read + 4-B ICRC written = frame bytes per packet
     out = {
         "workload": a.workload,
         "packets": n,
         "kernel": k_icrc,
         "fetch_size_raw_bytes": round(fetch_icrc_raw),
         "fetch_calibration": round(calib, 4),
-        "fetch_calibration_source": "stream_read_kernel over the same buffer: known bytes / FETCH_SIZE",
+        "fetch_calibration_source": f"{a.ceiling} in the same run: known bytes read / FETCH_SIZE",
         "fetch_bytes": round(fetch_icrc),
         "write_bytes": round(write_icrc),
         "traffic_bytes_per_launch": round(fetch_icrc + write_icrc),
         "alg_bytes_per_launch": alg,
         "traffic_over_alg": round((fetch_icrc + write_icrc) / alg, 4),
         "dispatches": {"fetch_pass": len(fr[k_icrc]["FETCH_SIZE"]),
-                       "write_pass": len(wr[pick(wr, "icrc_kernel")]["WRITE_SIZE"])},
+                       "write_pass": len(wr[pick(wr, a.kernel)]["WRITE_SIZE"])},
     }
-    Path(a.out).write_text(json.dumps(out, indent=1) + "\n")
+    Path(a.out or f"profiles/pmc_traffic_{a.workload}.json").write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out))
 
 

@@ -8,16 +8,17 @@ import sys
 from pathlib import Path
 
 d, bench_json = Path(sys.argv[1]), Path(sys.argv[2])
+needle = sys.argv[3] if len(sys.argv) > 3 else "icrc_kernel"
 stats = next(d.rglob("*kernel_stats.csv"))
 trace = next(d.rglob("*kernel_trace.csv"))
 print(f"== {stats.name}")
 print(stats.read_text().strip())
-rows = [r for r in csv.DictReader(open(trace)) if "icrc_kernel" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(trace)) if needle in r["Kernel_Name"]]
 durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
 bench = json.loads(bench_json.read_text().strip().splitlines()[-1])
 k = bench["steps"]
 timed = durs[-k:]
-print(f"== icrc_kernel dispatches: {len(durs)} (warmup {len(durs) - k} + timed {k})")
+print(f"== {needle} dispatches: {len(durs)} (warmup {len(durs) - k} + timed {k})")
 print(f"rocprof mean over timed dispatches: {sum(timed) / len(timed):.4f} ms "
       f"(min {min(timed):.4f}, max {max(timed):.4f})")
 print(f"bench HIP-event kernel_ms_mean:     {bench['kernel_ms_mean']:.4f} ms  "
