@@ -208,7 +208,9 @@ int ricrc_segment(ricrc_ctx* ctx, const uint8_t* mr, size_t mr_bytes, const ricr
  * (planned on the host, then copied) are device pointers; frames go to
  * d_frames + p * slot_bytes (slot_bytes: multiple of 256, >= the plan's;
  * d_frames 256-byte aligned).  d_lens doubles as the packet -> WR map while
- * the call runs. */
+ * the call runs.  WRs are validated on the device (status RICRC_PKT_SEG_BAD,
+ * length 0).  No byte outside [d_mr, d_mr + mr_bytes) is read, except that an
+ * MR shorter than 16 bytes must be readable for 16. */
 int ricrc_segment_dev(ricrc_ctx* ctx, const uint8_t* d_mr, uint64_t mr_bytes,
                       const ricrc_seg_wr* d_wrs, uint32_t nwr, uint32_t pmtu, uint32_t npkts,
                       uint8_t* d_frames, uint32_t slot_bytes, uint32_t* d_lens,

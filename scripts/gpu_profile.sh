@@ -8,10 +8,12 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
 make -C oracle -s || exit 1
-echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_$TAG.log 2>&1
-rc=$?; tail -5 $OUT/pytest_$TAG.log; echo "pytest rc=$rc"
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -z "${SKIP_TESTS:-}" ]; then
+  echo "== pytest -m gpu"
+  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_$TAG.log 2>&1
+  rc=$?; tail -5 $OUT/pytest_$TAG.log; echo "pytest rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+fi
 echo "== bench"
 timeout -k 10 600 python bench.py --workload $WL > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
 rc=$?; cat $OUT/bench_$TAG.json; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$TAG.err; exit $rc; }
@@ -39,7 +41,7 @@ else
     --packets $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][1])") \
     --frame-bytes $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][0] + 44)") \
     --out $OUT/pmc_traffic_${TAG}_$WL.json || exit 1
-  KN=icrc_kernel
+  KN=::icrc_
 fi
 python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json $KN > $OUT/prof_summary_$TAG.txt || exit 1
 cat $OUT/prof_summary_$TAG.txt

@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--packets", type=int, required=True)
     ap.add_argument("--frame-bytes", type=int, required=True)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--kernel", default="icrc_kernel")
+    ap.add_argument("--kernel", default="::icrc_")
     ap.add_argument("--ceiling", default="stream_read_kernel")
     ap.add_argument("--ceiling-read-bytes", type=int, default=0)
     ap.add_argument("--alg-bytes", type=int, default=0)

@@ -8,7 +8,7 @@ import sys
 from pathlib import Path
 
 d, bench_json = Path(sys.argv[1]), Path(sys.argv[2])
-needle = sys.argv[3] if len(sys.argv) > 3 else "icrc_kernel"
+needle = sys.argv[3] if len(sys.argv) > 3 else "::icrc_"
 stats = next(d.rglob("*kernel_stats.csv"))
 trace = next(d.rglob("*kernel_trace.csv"))
 print(f"== {stats.name}")
