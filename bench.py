@@ -110,20 +110,25 @@ def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: 
     _CPU_JOB = (buf, offs, lens)
     step = (n + procs * 4 - 1) // (procs * 4)
     chunks = [(s, min(n, s + step)) for s in range(0, n, step)]
-    t0 = time.perf_counter()
+    # passes over the whole batch until ~1 s of pool time (about 16 core-seconds)
+    passes, tn = 0, 0.0
     with mp.get_context("fork").Pool(procs) as pool:
-        parts = pool.map(_cpu_chunk, chunks)
-    tn = time.perf_counter() - t0
+        while passes == 0 or (tn < 1.0 and passes < 16):
+            t0 = time.perf_counter()
+            parts = pool.map(_cpu_chunk, chunks)
+            tn += time.perf_counter() - t0
+            passes += 1
     allc = np.concatenate(parts)
     mism = int((allc != gpu_icrc).sum()) + int((one != gpu_icrc[:n1]).sum())
     c_all, c_one = int(cov.sum()), int(cov[:n1].sum())
     return {
-        "value": round(c_all / tn / 2**30, 4),
+        "value": round(passes * c_all / tn / 2**30, 4),
         "unit": "GiB/s",
         "cores": procs,
         "kind": "port",
         "sample": (f"Python zlib.crc32 restatement of BTH.compute_icrc per packet over the same "
-                   f"host frames: {n} packets on a {procs}-process fork pool ({tn:.2f} s); "
+                   f"host frames: {passes} pass(es) over {n} packets on a {procs}-process fork "
+                   f"pool ({tn:.2f} s); "
                    f"single core {n1} packets {c_one / t1 / 2**30:.3f} GiB/s"),
         "single_core_GiBps": round(c_one / t1 / 2**30, 4),
         "parity_mismatches_vs_gpu": mism,
