@@ -46,7 +46,8 @@ WORKLOADS = {
              "64-B payload SEND_MIDDLE-shaped frames (108 B), ICRC compute, stride 108"),
     "cfg3": (0, 1 << 20, 0x1C2C0003,
              "mixed-MTU {256..4096} RDMA_WRITE_MIDDLE frames packed back to back, ICRC verify "
-             "(1/1024 payload bit flips must fail, 1/1024 randomised masked fields must pass)"),
+             "(GPU fault injector hits ~3/1024 frames: ICRC and payload bit flips must fail, "
+             "randomised masked fields must pass)"),
     # SURVEY 8(f) rows 1 + 3: frames built on the GPU from the MR, ICRC fused
     "seg": (4096, 1 << 20, 0x1C2C0006,
             "RC SEND of 256 KiB messages from a device MR, 4 KiB PMTU (FIRST + 62 MIDDLE + "
@@ -177,12 +178,15 @@ class Strided:
 class RaggedVerify:
     """cfg3: mixed-MTU frames packed back to back, ICRC verify.  Trailers are
     filled by the engine's compute path on the device (its parity is the test
-    suite's job), then 1/1024 frames get a payload bit flip (must fail) and
-    1/1024 get random masked-field values (must pass)."""
+    suite's job), then the GPU fault injector (ricrc_inject_faults_dev) hits
+    ~3/1024 frames: ICRC bit flips and payload bit flips (must fail) and
+    randomised masked fields (must pass)."""
 
     mode = "verify"
+    FAULT_PPM = 2930  # ~3 / 1024
 
     def __init__(self, torch, eng, dev, payload, n, seed, rank, world):
+        from roce_icrc import engine as E
         from roce_icrc import synth
         self.torch, self.eng, self.n = torch, eng, n
         self.buf, self.offs, self.lens = synth.mixed_mtu_frames(
@@ -199,18 +203,10 @@ class RaggedVerify:
         trail = (self.d_offs + self.d_lens.to(torch.int64) - 4)
         idx = trail[:, None] + torch.arange(4, device=dev)[None, :]
         self.d_frames[idx.reshape(-1)] = self.icrc.view(torch.uint8).reshape(-1)
-        rng = np.random.Generator(np.random.PCG64(seed + 17))
-        sel = rng.choice(n, size=2 * max(1, n // 1024), replace=False)
-        self.flip, self.masked = np.sort(sel[: len(sel) // 2]), np.sort(sel[len(sel) // 2:])
-        pay_off = self.offs[self.flip].astype(np.int64) + 40 + rng.integers(
-            0, self.lens[self.flip].astype(np.int64) - 44)
-        bits = torch.from_numpy(1 << rng.integers(0, 8, self.flip.size)).to(dev).to(torch.uint8)
-        p = torch.from_numpy(pay_off).to(dev)
-        self.d_frames[p] ^= bits
-        for k in (1, 8, 10, 11, 26, 27, 32):
-            p = torch.from_numpy(self.offs[self.masked].astype(np.int64) + k).to(dev)
-            v = torch.from_numpy(rng.integers(0, 256, self.masked.size).astype(np.uint8)).to(dev)
-            self.d_frames[p] = v
+        self.fault = torch.zeros(n, dtype=torch.uint8, device=dev)
+        eng.inject_faults_dev(self.d_frames, self.d_offs, self.d_lens, n, seed + 17,
+                              self.FAULT_PPM, E.FAULT_ICRC | E.FAULT_PAYLOAD | E.FAULT_MASKED,
+                              self.fault, stream=sp)
         torch.cuda.synchronize(dev)
         self.buf = self.d_frames.cpu().numpy()  # host copy with trailers + corruptions
 
@@ -228,11 +224,15 @@ class RaggedVerify:
         return "ragged default (8 at the mixed-MTU mean)"
 
     def check(self):
+        from roce_icrc import engine as E
         ok = self.ok.cpu().numpy().astype(bool)
+        fault = self.fault.cpu().numpy()
+        expect = ~np.isin(fault, [E.FAULT_ICRC, E.FAULT_PAYLOAD])
         return {"verify_ok": int(ok.sum()), "verify_failed": int((~ok).sum()),
-                "flipped_all_failed": bool((~ok[self.flip]).all()),
-                "masked_all_passed": bool(ok[self.masked].all()),
-                "expected_failures": int(self.flip.size)}
+                "faults": {"icrc": int((fault == E.FAULT_ICRC).sum()),
+                           "payload": int((fault == E.FAULT_PAYLOAD).sum()),
+                           "masked": int((fault == E.FAULT_MASKED).sum())},
+                "verdict_matches_injected": bool((ok == expect).all())}
 
 
 SEG_MSG = 256 * 1024

@@ -217,6 +217,29 @@ int ricrc_segment_dev(ricrc_ctx* ctx, const uint8_t* d_mr, uint64_t mr_bytes,
                       uint32_t* d_icrc /* nullable */, uint8_t* d_status /* nullable */,
                       void* stream);
 
+/* ---- ICRC fault injection -------------------------------------------------
+ *
+ *   reference                                        replaced by
+ *   -----------------------------------------------  -----------------------------
+ *   hook functions  src/hooks.py:10-138, registered  ricrc_inject_faults_dev: the
+ *     by SideServicer.SetHook src/sanity_side.py:     ICRC error case the reference
+ *     345-364 (they edit BTH/RETH/AETH/payload of     lacks, for whole batches;
+ *     one packet before it is built)                  roce_icrc.hooks for one packet
+ *
+ * Corrupts, in place, the frames of a seed-determined subset of a batch:
+ * packet i is hit when splitmix64(seed ^ i * 0xD1B54A32D192ED03) mod 10^6 <
+ * rate_ppm, with one of the kinds enabled in `kinds` (drawn from the same
+ * hash).  d_fault_out[i] = the kind applied, 0 for none (frames that are not
+ * well-formed IPv4 are never hit).  Expected verify outcome: ok unless the
+ * kind is ICRC or PAYLOAD. */
+#define RICRC_FAULT_ICRC 0x1    /* flip one bit of the 4-byte ICRC trailer             */
+#define RICRC_FAULT_PAYLOAD 0x2 /* flip one bit of a covered byte the ICRC does not mask */
+#define RICRC_FAULT_MASKED 0x4  /* randomise IP tos/ttl/checksum, UDP checksum, BTH
+                                   fecn|becn|resv6: the ICRC must not change         */
+int ricrc_inject_faults_dev(ricrc_ctx* ctx, uint8_t* d_frames, const uint64_t* d_offsets,
+                            const uint32_t* d_lens, uint32_t n, uint64_t seed, uint32_t rate_ppm,
+                            uint32_t kinds, uint8_t* d_fault_out /* nullable */, void* stream);
+
 /* ---- measurement -------------------------------------------------------- */
 /* STREAM-style copy of `bytes` (multiple of 16) from d_src to d_dst with
  * 16-B loads and stores: the read+write denominator of the segmentation

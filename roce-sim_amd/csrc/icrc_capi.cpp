@@ -559,6 +559,24 @@ int ricrc_segment_dev(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes,
                     d_icrc, d_status, pick_stream(c, stream));
 }
 
+int ricrc_inject_faults_dev(ricrc_ctx* c, uint8_t* d_frames, const uint64_t* d_offsets,
+                            const uint32_t* d_lens, uint32_t n, uint64_t seed, uint32_t rate_ppm,
+                            uint32_t kinds, uint8_t* d_fault_out, void* stream) {
+  if (!c || rate_ppm > 1000000u || (n && (!d_frames || !d_offsets || !d_lens))) return RICRC_EINVAL;
+  ricrc::FaultArgs a{};
+  a.frames = d_frames;
+  a.offsets = d_offsets;
+  a.lens = d_lens;
+  a.n = n;
+  a.seed = seed;
+  a.rate_ppm = rate_ppm;
+  a.kinds = kinds;
+  a.fault_out = d_fault_out;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ricrc::launch_faults(a, c->num_cus, pick_stream(c, stream)));
+  return RICRC_OK;
+}
+
 int ricrc_stream_copy_dev(ricrc_ctx* c, const uint8_t* d_src, uint8_t* d_dst, uint64_t bytes,
                           void* stream) {
   if (!c || !d_src || !d_dst || (bytes & 15)) return RICRC_EINVAL;

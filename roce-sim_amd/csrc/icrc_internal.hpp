@@ -70,3 +70,21 @@ hipError_t launch_stream_copy(const uint8_t* src, uint8_t* dst, uint64_t bytes, 
                               hipStream_t stream);
 
 }  // namespace ricrc
+
+namespace ricrc {
+
+struct FaultArgs {
+  uint8_t* frames;
+  const uint64_t* offsets;
+  const uint32_t* lens;
+  uint32_t n;
+  uint64_t seed;
+  uint32_t rate_ppm;
+  uint32_t kinds;
+  uint8_t* fault_out;  // nullable
+};
+
+// Enqueues the fault-injection kernel.
+hipError_t launch_faults(const FaultArgs& a, int num_cus, hipStream_t stream);
+
+}  // namespace ricrc

@@ -37,6 +37,9 @@ SEG_SEND, SEG_SEND_WITH_IMM, SEG_SEND_WITH_INV = 0, 1, 2
 SEG_RDMA_WRITE, SEG_RDMA_WRITE_WITH_IMM, SEG_READ_RESPONSE = 3, 4, 5
 SEG_SIGNALED, SEG_SOLICITED = 0x1, 0x2
 
+# fault kinds (RICRC_FAULT_*)
+FAULT_ICRC, FAULT_PAYLOAD, FAULT_MASKED = 0x1, 0x2, 0x4
+
 # struct ricrc_seg_wr (include/roce_icrc.h), 64 bytes, as a numpy record so
 # large WR batches are built vectorised
 SEG_WR_DTYPE = np.dtype([
@@ -121,6 +124,11 @@ _SIGNATURES = {
          ctypes.c_uint32, _vp, _vp, _vp, _vp],
     ),
     "ricrc_stream_copy_dev": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    "ricrc_inject_faults_dev": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+         _vp, _vp],
+    ),
 }
 
 _lib = None
@@ -333,6 +341,13 @@ class IcrcEngine:
         self._check("ricrc_segment_dev", self.lib.ricrc_segment_dev(
             self.ctx, _ptr(d_mr), mr_bytes, _ptr(d_wrs), nwr, pmtu, npkts, _ptr(d_frames), slot,
             _ptr(d_lens), _ptr(d_icrc), _ptr(d_status), stream))
+
+    def inject_faults_dev(self, d_frames, d_offsets, d_lens, n, seed, rate_ppm, kinds,
+                          d_fault_out=None, stream=None):
+        """Corrupt a seed-determined subset of frames in place (RICRC_FAULT_*)."""
+        self._check("ricrc_inject_faults_dev", self.lib.ricrc_inject_faults_dev(
+            self.ctx, _ptr(d_frames), _ptr(d_offsets), _ptr(d_lens), n, seed, rate_ppm, kinds,
+            _ptr(d_fault_out), stream))
 
     def stream_copy_dev(self, d_src, d_dst, nbytes, stream=None):
         self._check("ricrc_stream_copy_dev", self.lib.ricrc_stream_copy_dev(

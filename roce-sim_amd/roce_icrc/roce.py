@@ -319,13 +319,18 @@ class BTH(Packet):
         ("dqpn", 24, 0), ("ackreq", 1, 0), ("resv7", 7, 0), ("psn", 24, 0),
     ]
 
-    def __init__(self, _pkt=None, icrc: Optional[int] = None, **kw):
+    def __init__(self, _pkt=None, icrc: Optional[int] = None, icrc_fault: int = 0, **kw):
         self.__dict__["icrc"] = icrc
+        # XOR mask applied to the ICRC computed at build (0 = none): the ICRC
+        # error case of the hooks framework (roce_icrc.hooks), which the
+        # reference cannot express because it never checks the ICRC
+        self.__dict__["icrc_fault"] = icrc_fault
         super().__init__(_pkt, **kw)
 
     def copy(self):
         c = super().copy()
         c.__dict__["icrc"] = self.icrc
+        c.__dict__["icrc_fault"] = self.icrc_fault
         return c
 
     @staticmethod
@@ -349,7 +354,7 @@ class BTH(Packet):
             return self.pack_icrc(0)
         frame = wire_frame(ip, udp, p)
         icrc, status = get_engine().compute_one(frame)
-        return self.pack_icrc(icrc)
+        return self.pack_icrc(icrc ^ self.icrc_fault)
 
     def build_payload(self):
         trailer = struct.pack("!I", (self.icrc or 0) & 0xFFFFFFFF)  # FCSField "!I"
@@ -547,7 +552,7 @@ def emit_batch(pkts: list[Packet]) -> list[bytes]:
         icrc, _ = get_engine().compute_batch(np.frombuffer(b"".join(parts), np.uint8), offs, lens)
         for j, i in enumerate(need):
             f = bytearray(frames[i])
-            f[-4:] = BTH.pack_icrc(int(icrc[j]))
+            f[-4:] = BTH.pack_icrc(int(icrc[j]) ^ pkts[i][BTH].icrc_fault)
             ip = pkts[i].getlayer(IP)
             udp = pkts[i].getlayer(UDP)
             ihl = 4 * (f[0] & 0xF)
