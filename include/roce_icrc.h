@@ -80,7 +80,10 @@ int ricrc_device_count(int* count);
  * non-blocking stream, builds the GF(2) folding tables and uploads them. */
 int ricrc_ctx_create(int device, ricrc_ctx** out);
 void ricrc_ctx_destroy(ricrc_ctx* ctx);
-/* Lanes cooperating on one packet (1,2,4,...,64); 0 = automatic by length. */
+/* Lanes cooperating on one packet (1,2,4,...,64); 0 = automatic by length
+ * (strided frames with stride <= 128 bytes, a multiple of 4, then use the
+ * lane-per-packet kernel with LDS-staged loads; any non-zero setting forces
+ * the lane-group kernels). */
 int ricrc_ctx_set_lanes_per_packet(ricrc_ctx* ctx, int lanes);
 /* The hipStream_t the synchronous host-buffer calls run on. */
 void* ricrc_ctx_stream(ricrc_ctx* ctx);
@@ -250,7 +253,8 @@ int ricrc_stream_copy_dev(ricrc_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, 
  * loads, XOR-folded into d_sink[0]: the HBM-read denominator for the roofline. */
 int ricrc_stream_read_dev(ricrc_ctx* ctx, const uint8_t* d_buf, uint64_t bytes,
                           uint32_t* d_sink, void* stream);
-/* Lanes per packet the engine would use for frames of `len` bytes. */
+/* Lanes per packet the engine would use for frames of `len` bytes (1 for the
+ * lane-per-packet kernel of small strided frames). */
 int ricrc_lanes_for_len(ricrc_ctx* ctx, uint32_t len);
 
 #ifdef __cplusplus

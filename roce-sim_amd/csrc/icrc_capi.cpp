@@ -124,6 +124,13 @@ int ensure_pkts(ricrc_ctx* c, size_t n) {
   return RICRC_OK;
 }
 
+// Strided frames this small go to the lane-per-packet kernel (automatic lanes
+// only; an explicit lanes setting forces the lane-group kernels).
+bool use_small(const ricrc_ctx* c, uint64_t stride, uint32_t len) {
+  return c->lanes == 0 && stride <= ricrc::kSmallMaxStride && stride % 4 == 0 && len <= stride &&
+         len >= 4;
+}
+
 int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint32_t* lens,
            uint64_t stride, uint32_t len, uint32_t n, uint32_t* icrc, uint8_t* status, uint8_t* ok,
            bool ragged, bool verify, int log2g, hipStream_t s) {
@@ -139,7 +146,10 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   a.ok_out = ok;
   a.tables = c->d_tables;
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
+  if (!ragged && n > 0 && use_small(c, stride, len))
+    HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
+  else
+    HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
   return RICRC_OK;
 }
 
@@ -325,6 +335,7 @@ void* ricrc_ctx_stream(ricrc_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int ricrc_lanes_for_len(ricrc_ctx* c, uint32_t len) {
   if (!c) return RICRC_EINVAL;
+  if (use_small(c, len, len)) return 1;  // lane-per-packet kernel (strided, stride = len)
   return 1 << pick_log2g(c, len);
 }
 

@@ -12,7 +12,10 @@ namespace ricrc {
 constexpr int kMaxLog2G = 6;
 constexpr int kNumMainSets = kMaxLog2G + 1;
 constexpr int kNumCombSets = kMaxLog2G + 1;
-constexpr int kTableWords = (kNumMainSets + kNumCombSets) * 1024;
+// ... then one Mul(32) set: the per-dword step of the lane-per-packet kernel
+// for small frames.
+constexpr int kSmallSet = kNumMainSets + kNumCombSets;
+constexpr int kTableWords = (kNumMainSets + kNumCombSets + 1) * 1024;
 
 struct IcrcArgs {
   const uint8_t* frames;
@@ -33,6 +36,11 @@ void build_table_image(uint32_t* out);
 // Enqueues the ICRC kernel; returns a hipError_t.
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
                        hipStream_t stream);
+
+// Strided frames of at most kSmallMaxStride bytes (stride a multiple of 4):
+// the lane-per-packet kernel with LDS-staged, coalesced loads.
+constexpr uint32_t kSmallMaxStride = 128;
+hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream);
 
 // Enqueues the STREAM-style read kernel (roofline denominator).
 hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, int num_cus,

@@ -413,6 +413,129 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Small frames (strided, stride <= kSmallMaxStride): one LANE per packet.
+//
+// With a group of lanes per packet, a 108-byte frame gives each lane a dozen
+// dwords against a fixed per-packet cost (describe, head fix-ups, rotation,
+// combine) of several hundred instructions.  Here a wave takes a batch of 64
+// consecutive packets: their 64 x stride bytes arrive with fully coalesced
+// 16-byte loads (issued two batches ahead, held in registers), go to the
+// wave's LDS staging slot, and each lane then folds its own frame serially,
+// r <- Mul(32)(r ^ w), reading its dwords from LDS and the Mul(32) set from
+// the same 32x-replicated, conflict-free layout as the grid kernels.  No
+// cross-lane combine.  The batch holding the last packet reads its frames
+// straight from global memory (no 16-byte over-read past the buffer).
+//
+// LDS: [0, 128 KiB) Mul(32) tables; then kSmallWaves x 64 x stride bytes.
+constexpr int kSmallWaves = 4;
+
+template <int C, bool VERIFY>
+__global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArgs a) {
+  const int tid = threadIdx.x;
+  stage_main_set(a.tables + kSmallSet * 1024, tid, 64 * kSmallWaves);
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  const uint32_t kc0 = (uint32_t)(lane & 31) << 2, kc1 = kc0 | 0x10000u;
+  const uint32_t S = (uint32_t)a.stride, L = a.len;
+  const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch
+  const uint32_t stage = kLdsMain + (uint32_t)wave * 64u * S;
+  const uint32_t nb = (a.n + 63) / 64;
+  const uint32_t last = nb - 1;  // the batch holding packet n-1: direct path
+  const uint32_t per_block = (nb + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * per_block, b1 = min(nb, b0 + per_block);
+  const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
+  const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform)
+
+  // fold this lane's frame (dword k = rd(k)) and emit its outputs
+  auto packet = [&](uint32_t pkt, bool live, auto rd) {
+    const uint32_t d0 = rd(0), d2 = rd(2);
+    uint32_t st = dead ? kPktBadLen : 0u;
+    const int ihl = (int)(d0 & 0xFu);
+    if (st == 0) {
+      if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
+        st |= kPktNotIpv4;
+      else if (((d2 >> 8) & 0xFFu) != 17u)
+        st |= kPktNotUdp;
+      else if (L < (uint32_t)(4 * ihl + 24))
+        st |= kPktBadLen;
+      const uint32_t tot = ((d0 >> 8) & 0xFF00u) | (d0 >> 24);
+      if (tot != L) st |= kPktLenMismatch;
+    }
+    const bool good = (st & kPktFatal) == 0;
+    uint32_t P = 0, T = 0;
+    if (__all(!live || (good && ihl == 5))) {
+      // IHL 5 everywhere: the masks sit at fixed dwords (uniform k)
+      absorb(P, T, (rd(0) | 0x0000FF00u) ^ kSeedRegister, kc0, kc1);
+      absorb(P, T, rd(1), kc0, kc1);
+      absorb(P, T, rd(2) | 0xFFFF00FFu, kc0, kc1);
+      absorb(P, T, rd(3), kc0, kc1);
+      absorb(P, T, rd(4), kc0, kc1);
+      absorb(P, T, rd(5), kc0, kc1);
+      absorb(P, T, rd(6) | 0xFFFF0000u, kc0, kc1);
+      absorb(P, T, rd(7), kc0, kc1);
+      absorb(P, T, rd(8) | 0x000000FFu, kc0, kc1);
+#pragma unroll 4
+      for (int k = 9; k < n; ++k) absorb(P, T, rd(k), kc0, kc1);
+    } else {
+      for (int k = 0; k < n; ++k) absorb(P, T, fix_dword(rd(k), k, ihl + 1, ihl + 3), kc0, kc1);
+    }
+    const uint32_t icrc = good ? ~(P ^ T) : 0u;
+    if (live) {
+      if constexpr (VERIFY) {
+        const bool ok = good && rd(n) == icrc;
+        if (good && !ok) st |= kPktIcrcMismatch;
+        a.ok_out[pkt] = ok ? 1 : 0;
+      }
+      if (a.icrc_out) a.icrc_out[pkt] = icrc;
+      if (a.status_out) a.status_out[pkt] = (uint8_t)st;
+    }
+  };
+  auto load = [&](uint32_t b, u32x4* R) {  // unconditional: clamped chunk index
+    const uint8_t* base = a.frames + (uint64_t)min(b, last - 1) * 64u * S;
+#pragma unroll
+    for (int t = 0; t < C; ++t) R[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
+  };
+  auto stage_and_fold = [&](uint32_t b, const u32x4* R) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+      const uint32_t c = (uint32_t)(lane + 64 * t);
+      if (c < nchunk) *(lds_u32x4*)(uintptr_t)(stage + 16u * c) = R[t];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t pb = stage + (uint32_t)lane * S;
+    packet(b * 64u + (uint32_t)lane, true, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // staged batches [b0 + wave, min(b1, last)) step kSmallWaves, two in flight
+  const uint32_t bs_end = min(b1, last);
+  if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
+    u32x4 X[C], Y[C];
+    uint32_t b = b0 + (uint32_t)wave;
+    load(b, X);
+    load(b + kSmallWaves, Y);
+    for (; b < bs_end; b += 2 * kSmallWaves) {
+      stage_and_fold(b, X);
+      load(b + 2 * kSmallWaves, X);
+      if (b + kSmallWaves >= bs_end) break;
+      stage_and_fold(b + kSmallWaves, Y);
+      load(b + 3 * kSmallWaves, Y);
+    }
+  }
+  // the last batch, straight from global memory (one wave of the owning block)
+  if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % kSmallWaves) {
+    const uint32_t pkt = last * 64u + (uint32_t)lane;
+    const bool live = pkt < a.n;
+    const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
+    packet(pkt, live, [&](int k) { return ldg32(f + 4 * k); });
+  }
+}
+
 // STREAM-style read ceiling with the same geometry as the ICRC kernel: one
 // 1024-thread workgroup per CU sweeping a contiguous chunk, 16-B nt loads.
 __global__ void __launch_bounds__(1024) stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
@@ -476,6 +599,7 @@ void build_table_image(uint32_t* out) {
   uint32_t* comb = out + kNumMainSets * 1024;
   table_set(-32, comb);
   for (int l = 0; l < kMaxLog2G; ++l) table_set(-(128ll << l), comb + (1 + l) * 1024);
+  table_set(32, out + kSmallSet * 1024);
 }
 
 hipError_t prepare_kernels() {
@@ -501,6 +625,30 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), lds_bytes(log2g, ragged), stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  if (a.stride > kSmallMaxStride || (a.stride & 3u) || a.stride == 0) return hipErrorInvalidValue;
+  const int C = a.stride <= 64 ? 4 : 8;  // 16-byte loads per lane per batch (4 * stride / 64)
+  kernel_fn k = C == 4 ? (verify ? icrc_small_kernel<4, true> : icrc_small_kernel<4, false>)
+                       : (verify ? icrc_small_kernel<8, true> : icrc_small_kernel<8, false>);
+  const size_t lds = kLdsMain + (size_t)kSmallWaves * 64u * a.stride;
+  static const hipError_t prep = [] {
+    for (void* f : {(void*)icrc_small_kernel<4, true>, (void*)icrc_small_kernel<4, false>,
+                    (void*)icrc_small_kernel<8, true>, (void*)icrc_small_kernel<8, false>}) {
+      hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(kLdsMain + kSmallWaves * 64u * kSmallMaxStride));
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }();
+  if (prep != hipSuccess) return prep;
+  const uint64_t nb = (a.n + 63) / 64;
+  uint64_t blocks = (nb + kSmallWaves - 1) / kSmallWaves;
+  if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kSmallWaves), lds, stream, a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,98 @@
+"""GPU parity of the lane-per-packet kernel for small strided frames
+(stride <= 128 B, automatic lanes): batch boundaries, strides with gaps,
+IPv4 options (the generic-mask path), malformed frames, verify mode, and
+agreement with the lane-group kernels on the same bytes."""
+import numpy as np
+import pytest
+
+import icrc_oracle as o
+from conftest import oracle_batch
+from roce_icrc.engine import PKT_ICRC_MISMATCH, PKT_NOT_IPV4
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame(L, rng, ihl6=False):
+    pay = L - 44 - (4 if ihl6 else 0)
+    f = bytearray(o.build_frame("10.0.0.1", "10.0.0.2", int(rng.integers(1 << 16)),
+                                dict(opcode=0x01, psn=int(rng.integers(1 << 24)), dqpn=0x11),
+                                payload=rng.integers(0, 256, pay, dtype=np.uint8).tobytes()))
+    if ihl6:  # insert one dword of IPv4 options; lengths follow
+        f = f[:20] + bytearray(b"\x01\x01\x01\x00") + f[20:]
+        f[0] = 0x46
+        f[2:4] = len(f).to_bytes(2, "big")
+    assert len(f) == L
+    return bytes(f)
+
+
+def _strided(n, L, stride, rng, ihl6_every=0, bad_every=0):
+    buf = np.zeros((n - 1) * stride + L, np.uint8)
+    for i in range(n):
+        f = _frame(L, rng, ihl6=bool(ihl6_every and i % ihl6_every == 3))
+        if bad_every and i % bad_every == 5:
+            f = b"\x60" + f[1:]  # IPv6 version nibble -> not IPv4
+        buf[i * stride: i * stride + L] = np.frombuffer(f, np.uint8)
+    return buf
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 1023, 4099])
+@pytest.mark.parametrize("L,stride", [(48, 48), (108, 108), (108, 112), (64, 128), (128, 128)])
+def test_small_kernel_matches_oracle(engine, n, L, stride):
+    rng = np.random.default_rng(n * 1000 + L + stride)
+    buf = _strided(n, L, stride, rng)
+    assert engine.lanes_for_len(L) == 1
+    got, st = engine.compute_strided(buf, stride, L, n)
+    want, _ = oracle_batch(buf, stride=stride, length=L, n=n)
+    np.testing.assert_array_equal(got, want)
+    assert not st.any()
+
+
+def test_ipv4_options_and_malformed_frames(engine):
+    n, L, stride = 3000, 108, 108
+    rng = np.random.default_rng(1)
+    buf = _strided(n, L, stride, rng, ihl6_every=7, bad_every=11)
+    got, st = engine.compute_strided(buf, stride, L, n)
+    want = np.array([o.icrc_of_frame(bytes(buf[i * stride: i * stride + L])) or 0
+                     for i in range(n)], np.uint32)
+    bad = np.array([i % 11 == 5 for i in range(n)])
+    np.testing.assert_array_equal(got[~bad], want[~bad])
+    assert (got[bad] == 0).all() and (st[bad] & PKT_NOT_IPV4).all()
+    assert not st[~bad].any()
+
+
+def test_same_result_as_lane_group_kernels(engine):
+    n, L = 20000, 108
+    rng = np.random.default_rng(2)
+    buf = _strided(n, L, L, rng, ihl6_every=13, bad_every=17)
+    small, st_small = engine.compute_strided(buf, L, L, n)
+    engine.set_lanes(2)
+    try:
+        grid, st_grid = engine.compute_strided(buf, L, L, n)
+    finally:
+        engine.set_lanes(0)
+    np.testing.assert_array_equal(small, grid)
+    np.testing.assert_array_equal(st_small, st_grid)
+
+
+@pytest.mark.parametrize("n", [64, 1000, 100003])
+def test_small_kernel_verify(engine, n):
+    import torch
+    L = 108
+    rng = np.random.default_rng(n)
+    buf = _strided(n, L, L, rng)
+    icrc, _ = oracle_batch(buf, stride=L, length=L, n=n)
+    frames = buf.reshape(n, L)
+    frames[:, L - 4:] = icrc.astype("<u4").view(np.uint8).reshape(n, 4)
+    flip = rng.choice(n, size=max(1, n // 100), replace=False)
+    frames[flip, 50] ^= 0x10
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(buf).to(dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.verify_strided_dev(d, L, L, n, ok, None, st)
+    torch.cuda.synchronize()
+    okh, sth = ok.cpu().numpy().astype(bool), st.cpu().numpy()
+    want = np.ones(n, bool)
+    want[flip] = False
+    np.testing.assert_array_equal(okh, want)
+    assert (sth[flip] & PKT_ICRC_MISMATCH).all() and not sth[want].any()
