@@ -156,15 +156,6 @@ __device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n,
 }
 
 // LDS staging of the folding tables (every kernel, once per workgroup).
-// One table set `gm` (4 x 256 words) into [0, 128 KiB) in the replicated,
-// conflict-free layout absorb() reads, by a block of `nthreads` threads.
-__device__ __forceinline__ void stage_main_set(const uint32_t* gm, int tid, int nthreads) {
-  for (int i = tid; i < 8192; i += nthreads) {  // 8192 16-byte quads
-    const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
-    lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), gm[tab * 256 + e]);
-  }
-}
-
 template <int LOG2G>
 __device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
   constexpr int NCOMB = 1 + LOG2G;

@@ -421,37 +421,68 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
 // combine) of several hundred instructions.  Here a wave takes a batch of 64
 // consecutive packets: their 64 x stride bytes arrive with fully coalesced
 // 16-byte loads (issued two batches ahead, held in registers), go to the
-// wave's LDS staging slot, and each lane then folds its own frame serially,
-// r <- Mul(32)(r ^ w), reading its dwords from LDS and the Mul(32) set from
-// the same 32x-replicated, conflict-free layout as the grid kernels.  No
-// cross-lane combine.  The batch holding the last packet reads its frames
-// straight from global memory (no 16-byte over-read past the buffer).
+// wave's LDS staging slot, each lane patches its frame's masked dwords and
+// seed in place, and folds the frame from LDS.  The n covered dwords form
+// four independent chains (lengths q, q, q, n - 3q; r <- Mul(32)(r ^ w) each)
+// joined by Horner steps with Mul(32 q) and Mul(32 (n - 3q)).  The batch
+// holding the last packet reads its frames straight from global memory (no
+// 16-byte over-read past the buffer) in one chain.
 //
-// LDS: [0, 128 KiB) Mul(32) tables; then kSmallWaves x 64 x stride bytes.
-constexpr int kSmallWaves = 4;
+// Nothing between a batch's loads and their use may be predicated or fenced:
+// the compiler would then drain every load in flight (vmcnt(0)), including
+// the prefetch.  Hence unconditional LDS writes into a 64 x 16 x C-byte slot
+// and the masks applied in LDS rather than by uniform selects in the loop.
+//
+// LDS: [0, 64 KiB) Mul(32) replicated 16x (lanes l and l + 16 share a copy:
+// ~1.5-way conflicts), [64, 72 KiB) the two combine sets, then kSmallWaves
+// slots of 1024 C bytes.
+constexpr int kSmallWaves = 8;
+constexpr uint32_t kSmallComb = 65536;
+constexpr uint32_t kSmallStage = kSmallComb + 8192;
 
-template <int C, bool VERIFY>
+// Mul(32)(x) from the 16x-replicated set; kc = (lane & 15) * 4.
+__device__ __forceinline__ uint32_t mul32_rep16(uint32_t x, uint32_t kc) {
+  const uint32_t t0 = lds_rd(((x << 6) & 0x3FC0u) | kc);
+  const uint32_t t1 = lds_rd((((x >> 2) & 0x3FC0u) | kc) + 16384u);
+  const uint32_t t2 = lds_rd((((x >> 10) & 0x3FC0u) | kc) + 32768u);
+  const uint32_t t3 = lds_rd((((x >> 18) & 0x3FC0u) | kc) + 49152u);
+  return xor3(t0, t1, t2) ^ t3;
+}
+
+template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
-  stage_main_set(a.tables + kSmallSet * 1024, tid, 64 * kSmallWaves);
+  const uint32_t S = (uint32_t)a.stride, L = a.len;
+  const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
+  const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
+  const int q = n >> 2, rlen = n - 3 * q;        // chain lengths
+  {
+    const uint32_t* m32 = a.tables + kSmallSet * 1024;
+    for (int i = tid; i < 16384; i += 64 * kSmallWaves) {  // 16 copies of 1024 words
+      const int w = i >> 4, c = i & 15;
+      lds_wr((uint32_t)((w >> 8) * 16384 + (w & 255) * 64 + c * 4), m32[w]);
+    }
+    const uint32_t* cq = a.tables + (kSmallSet + max(q, 1) - 1) * 1024;
+    const uint32_t* cr = a.tables + (kSmallSet + max(rlen, 1) - 1) * 1024;
+    for (int i = tid; i < 1024; i += 64 * kSmallWaves) {
+      lds_wr(kSmallComb + 4u * i, cq[i]);
+      lds_wr(kSmallComb + 4096u + 4u * i, cr[i]);
+    }
+  }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  const uint32_t kc0 = (uint32_t)(lane & 31) << 2, kc1 = kc0 | 0x10000u;
-  const uint32_t S = (uint32_t)a.stride, L = a.len;
-  const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch
-  const uint32_t stage = kLdsMain + (uint32_t)wave * 64u * S;
+  const uint32_t kc = (uint32_t)(lane & 15) << 2;
+  const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch (<= 64 C)
+  const uint32_t stage = kSmallStage + (uint32_t)wave * 1024u * C;
   const uint32_t nb = (a.n + 63) / 64;
   const uint32_t last = nb - 1;  // the batch holding packet n-1: direct path
   const uint32_t per_block = (nb + gridDim.x - 1) / gridDim.x;
   const uint32_t b0 = blockIdx.x * per_block, b1 = min(nb, b0 + per_block);
-  const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
-  const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform)
 
-  // fold this lane's frame (dword k = rd(k)) and emit its outputs
-  auto packet = [&](uint32_t pkt, bool live, auto rd) {
-    const uint32_t d0 = rd(0), d2 = rd(2);
+  // header checks of one frame (dwords 0 and 2)
+  auto check = [&](uint32_t d0, uint32_t d2, int& ihl) {
     uint32_t st = dead ? kPktBadLen : 0u;
-    const int ihl = (int)(d0 & 0xFu);
+    ihl = (int)(d0 & 0xFu);
     if (st == 0) {
       if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
         st |= kPktNotIpv4;
@@ -462,77 +493,96 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
       const uint32_t tot = ((d0 >> 8) & 0xFF00u) | (d0 >> 24);
       if (tot != L) st |= kPktLenMismatch;
     }
+    return st;
+  };
+  auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer) {
     const bool good = (st & kPktFatal) == 0;
-    uint32_t P = 0, T = 0;
-    if (__all(!live || (good && ihl == 5))) {
-      // IHL 5 everywhere: the masks sit at fixed dwords (uniform k)
-      absorb(P, T, (rd(0) | 0x0000FF00u) ^ kSeedRegister, kc0, kc1);
-      absorb(P, T, rd(1), kc0, kc1);
-      absorb(P, T, rd(2) | 0xFFFF00FFu, kc0, kc1);
-      absorb(P, T, rd(3), kc0, kc1);
-      absorb(P, T, rd(4), kc0, kc1);
-      absorb(P, T, rd(5), kc0, kc1);
-      absorb(P, T, rd(6) | 0xFFFF0000u, kc0, kc1);
-      absorb(P, T, rd(7), kc0, kc1);
-      absorb(P, T, rd(8) | 0x000000FFu, kc0, kc1);
-#pragma unroll 4
-      for (int k = 9; k < n; ++k) absorb(P, T, rd(k), kc0, kc1);
-    } else {
-      for (int k = 0; k < n; ++k) absorb(P, T, fix_dword(rd(k), k, ihl + 1, ihl + 3), kc0, kc1);
-    }
-    const uint32_t icrc = good ? ~(P ^ T) : 0u;
+    const uint32_t icrc = good ? ~R : 0u;
     if (live) {
       if constexpr (VERIFY) {
-        const bool ok = good && rd(n) == icrc;
+        const bool ok = good && trailer == icrc;
         if (good && !ok) st |= kPktIcrcMismatch;
         a.ok_out[pkt] = ok ? 1 : 0;
       }
-      if (a.icrc_out) a.icrc_out[pkt] = icrc;
-      if (a.status_out) a.status_out[pkt] = (uint8_t)st;
+      if constexpr ((OUTS & 1) != 0) a.icrc_out[pkt] = icrc;
+      if constexpr ((OUTS & 2) != 0) a.status_out[pkt] = (uint8_t)st;
     }
   };
-  auto load = [&](uint32_t b, u32x4* R) {  // unconditional: clamped chunk index
+  // one chain over dwords [0, n) with per-lane masks (IPv4 options, the
+  // direct path, malformed frames)
+  auto one_chain = [&](int ihl, auto rd) {
+    uint32_t R = 0;
+    for (int k = 0; k < n; ++k) R = mul32_rep16(R ^ fix_dword(rd(k), k, ihl + 1, ihl + 3), kc);
+    return R;
+  };
+  auto load = [&](uint32_t b, u32x4* Rg) {  // unconditional: clamped chunk index
     const uint8_t* base = a.frames + (uint64_t)min(b, last - 1) * 64u * S;
 #pragma unroll
-    for (int t = 0; t < C; ++t) R[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
+    for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
   };
-  auto stage_and_fold = [&](uint32_t b, const u32x4* R) {
+  auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext) {
 #pragma unroll
-    for (int t = 0; t < C; ++t) {
-      const uint32_t c = (uint32_t)(lane + 64 * t);
-      if (c < nchunk) *(lds_u32x4*)(uintptr_t)(stage + 16u * c) = R[t];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = 0; t < C; ++t) *(lds_u32x4*)(uintptr_t)(stage + 16u * (uint32_t)(lane + 64 * t)) = Rg[t];
+    __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
+    load(bnext, Rg);  // the registers are free again: prefetch the next batch
     const uint32_t pb = stage + (uint32_t)lane * S;
-    packet(b * 64u + (uint32_t)lane, true, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+    int ihl;
+    uint32_t st = check(d0, d2, ihl);
+    uint32_t R;
+    if (__all((st & kPktFatal) == 0 && ihl == 5)) {
+      // IHL 5 everywhere: patch the masked dwords and the seed in place
+      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+      __asm__ __volatile__("" ::: "memory");
+      uint32_t A = 0, B = 0, Cc = 0, D = 0;
+      const uint32_t pa = pb, pbb = pb + 4u * q, pc = pb + 8u * q, pd = pb + 12u * q;
+      for (int j = 0; j < q; ++j) {
+        A = mul32_rep16(A ^ lds_rd(pa + 4u * j), kc);
+        B = mul32_rep16(B ^ lds_rd(pbb + 4u * j), kc);
+        Cc = mul32_rep16(Cc ^ lds_rd(pc + 4u * j), kc);
+        D = mul32_rep16(D ^ lds_rd(pd + 4u * j), kc);
+      }
+      for (int j = q; j < rlen; ++j) D = mul32_rep16(D ^ lds_rd(pd + 4u * j), kc);
+      R = mul_comb(A, kSmallComb) ^ B;
+      R = mul_comb(R, kSmallComb) ^ Cc;
+      R = mul_comb(R, kSmallComb + 4096u) ^ D;
+    } else {
+      R = one_chain(ihl, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
+    }
+    emit(b * 64u + (uint32_t)lane, true, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u);
+    __asm__ __volatile__("" ::: "memory");
   };
 
-  // staged batches [b0 + wave, min(b1, last)) step kSmallWaves, two in flight
+  // staged batches [b0 + wave, min(b1, last)) step kSmallWaves; each batch's
+  // loads are issued two batches ahead (buffers X, Y), right after the batch
+  // that used the buffer is staged
   const uint32_t bs_end = min(b1, last);
   if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
+    const uint32_t first = b0 + (uint32_t)wave;
+    const int cnt = first < bs_end ? (int)((bs_end - first + kSmallWaves - 1) / kSmallWaves) : 0;
     u32x4 X[C], Y[C];
-    uint32_t b = b0 + (uint32_t)wave;
-    load(b, X);
-    load(b + kSmallWaves, Y);
-    for (; b < bs_end; b += 2 * kSmallWaves) {
-      stage_and_fold(b, X);
-      load(b + 2 * kSmallWaves, X);
-      if (b + kSmallWaves >= bs_end) break;
-      stage_and_fold(b + kSmallWaves, Y);
-      load(b + 3 * kSmallWaves, Y);
+    load(first, X);
+    load(first + kSmallWaves, Y);
+    uint32_t b = first;
+    int i = 0;
+    for (; i + 1 < cnt; i += 2, b += 2 * kSmallWaves) {
+      stage_and_fold(b, X, b + 2 * kSmallWaves);
+      stage_and_fold(b + kSmallWaves, Y, b + 3 * kSmallWaves);
     }
+    if (i < cnt) stage_and_fold(b, X, b + 2 * kSmallWaves);
   }
   // the last batch, straight from global memory (one wave of the owning block)
   if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % kSmallWaves) {
     const uint32_t pkt = last * 64u + (uint32_t)lane;
     const bool live = pkt < a.n;
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
-    packet(pkt, live, [&](int k) { return ldg32(f + 4 * k); });
+    int ihl;
+    const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
+    const uint32_t R = one_chain(ihl, [&](int k) { return ldg32(f + 4 * k); });
+    emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
   }
 }
 
@@ -599,7 +649,7 @@ void build_table_image(uint32_t* out) {
   uint32_t* comb = out + kNumMainSets * 1024;
   table_set(-32, comb);
   for (int l = 0; l < kMaxLog2G; ++l) table_set(-(128ll << l), comb + (1 + l) * 1024);
-  table_set(32, out + kSmallSet * 1024);
+  for (int m = 1; m <= kSmallMaxDwords; ++m) table_set(32ll * m, out + (kSmallSet + m - 1) * 1024);
 }
 
 hipError_t prepare_kernels() {
@@ -628,20 +678,37 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   return hipGetLastError();
 }
 
+template <int C, bool V>
+kernel_fn pick_small(int outs) {
+  switch (outs) {
+    case 0: return icrc_small_kernel<C, V, 0>;
+    case 1: return icrc_small_kernel<C, V, 1>;
+    case 2: return icrc_small_kernel<C, V, 2>;
+    default: return icrc_small_kernel<C, V, 3>;
+  }
+}
+
+kernel_fn select_small(int C, bool verify, int outs) {
+  if (C == 4) return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
+  return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
+}
+
 hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   if (a.stride > kSmallMaxStride || (a.stride & 3u) || a.stride == 0) return hipErrorInvalidValue;
   const int C = a.stride <= 64 ? 4 : 8;  // 16-byte loads per lane per batch (4 * stride / 64)
-  kernel_fn k = C == 4 ? (verify ? icrc_small_kernel<4, true> : icrc_small_kernel<4, false>)
-                       : (verify ? icrc_small_kernel<8, true> : icrc_small_kernel<8, false>);
-  const size_t lds = kLdsMain + (size_t)kSmallWaves * 64u * a.stride;
+  const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
+  kernel_fn k = select_small(C, verify, outs);
+  const size_t lds = kSmallStage + (size_t)kSmallWaves * 1024u * C;
   static const hipError_t prep = [] {
-    for (void* f : {(void*)icrc_small_kernel<4, true>, (void*)icrc_small_kernel<4, false>,
-                    (void*)icrc_small_kernel<8, true>, (void*)icrc_small_kernel<8, false>}) {
-      hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)(kLdsMain + kSmallWaves * 64u * kSmallMaxStride));
-      if (e != hipSuccess) return e;
-    }
+    for (int c : {4, 8})
+      for (int v = 0; v < 2; ++v)
+        for (int o = 0; o < 4; ++o) {
+          hipError_t e = hipFuncSetAttribute((const void*)select_small(c, v, o),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)(kSmallStage + kSmallWaves * 1024u * 8));
+          if (e != hipSuccess) return e;
+        }
     return hipSuccess;
   }();
   if (prep != hipSuccess) return prep;
