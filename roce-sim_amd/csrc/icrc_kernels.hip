@@ -433,20 +433,47 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
 // the prefetch.  Hence unconditional LDS writes into a 64 x 16 x C-byte slot
 // and the masks applied in LDS rather than by uniform selects in the loop.
 //
-// LDS: [0, 64 KiB) Mul(32) replicated 16x (lanes l and l + 16 share a copy:
-// ~1.5-way conflicts), [64, 72 KiB) the two combine sets, then kSmallWaves
-// slots of 1024 C bytes.
+// LDS: [0, 64 KiB) Mul(32) replicated 16x, [64, 72 KiB) the two combine
+// sets, then kSmallWaves slots of 1024 C bytes.  Replica layout: entry e of
+// table t, copy c at e * 256 + t * 64 + c * 4 (c = lane & 15).  Lanes l and
+// l + 16 of a ds_read_b32 half-wave share copy c, so they read DIFFERENT
+// tables in each of the four lookups (lane half h = (lane >> 4) & 1 reads
+// table i ^ h in lookup i): table t sits on banks (t & 1) * 16 + c, and
+// i ^ h flips that parity, so the half-wave is conflict-free.  The XOR of
+// the four lookups is the same in any order.  Each address is ONE v_perm_b32
+// (x byte (i ^ h) -> byte 1, the per-lane copy/table offset -> byte 0) with
+// per-lane selector registers; the odd lookups' table offset is folded into
+// their own constant, the upper pair's 128 into the instruction offset.
 constexpr int kSmallWaves = 8;
 constexpr uint32_t kSmallComb = 65536;
 constexpr uint32_t kSmallStage = kSmallComb + 8192;
 
-// Mul(32)(x) from the 16x-replicated set; kc = (lane & 15) * 4.
-__device__ __forceinline__ uint32_t mul32_rep16(uint32_t x, uint32_t kc) {
-  const uint32_t t0 = lds_rd(((x << 6) & 0x3FC0u) | kc);
-  const uint32_t t1 = lds_rd((((x >> 2) & 0x3FC0u) | kc) + 16384u);
-  const uint32_t t2 = lds_rd((((x >> 10) & 0x3FC0u) | kc) + 32768u);
-  const uint32_t t3 = lds_rd((((x >> 18) & 0x3FC0u) | kc) + 49152u);
-  return xor3(t0, t1, t2) ^ t3;
+struct SmallKeys {
+  uint32_t ke, ko;              // byte 0: c * 4 + h * 64, c * 4 + (1 - h) * 64
+  uint32_t s0, s1, s2, s3;      // v_perm selectors: x byte (i ^ h) -> byte 1
+};
+
+__device__ __forceinline__ SmallKeys small_keys(int lane) {
+  const uint32_t c = (uint32_t)(lane & 15), h = (uint32_t)(lane >> 4) & 1u;
+  SmallKeys k;
+  k.ke = c * 4u + h * 64u;
+  k.ko = c * 4u + (1u - h) * 64u;
+  k.s0 = 0x0C0C0000u | ((4u + (0u ^ h)) << 8);
+  k.s1 = 0x0C0C0000u | ((4u + (1u ^ h)) << 8);
+  k.s2 = 0x0C0C0000u | ((4u + (2u ^ h)) << 8);
+  k.s3 = 0x0C0C0000u | ((4u + (3u ^ h)) << 8);
+  return k;
+}
+
+// (P, T) <- Mul(32)(P ^ T ^ w) from the 16x set (P = three lookups, T = the fourth)
+__device__ __forceinline__ void absorb16(uint32_t& P, uint32_t& T, uint32_t w, const SmallKeys& k) {
+  const uint32_t x = xor3(P, T, w);
+  const uint32_t a0 = __builtin_amdgcn_perm(x, k.ke, k.s0);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, k.ko, k.s1);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, k.ke, k.s2);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, k.ko, k.s3);
+  P = xor3(lds_rd(a0), lds_rd(a1), lds_rd(a2 + 128u));
+  T = lds_rd(a3 + 128u);
 }
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
@@ -459,8 +486,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
   {
     const uint32_t* m32 = a.tables + kSmallSet * 1024;
     for (int i = tid; i < 16384; i += 64 * kSmallWaves) {  // 16 copies of 1024 words
-      const int w = i >> 4, c = i & 15;
-      lds_wr((uint32_t)((w >> 8) * 16384 + (w & 255) * 64 + c * 4), m32[w]);
+      const int w = i >> 4, c = i & 15;  // w = t * 256 + e
+      lds_wr((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + c * 4), m32[w]);
     }
     const uint32_t* cq = a.tables + (kSmallSet + max(q, 1) - 1) * 1024;
     const uint32_t* cr = a.tables + (kSmallSet + max(rlen, 1) - 1) * 1024;
@@ -471,7 +498,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  const uint32_t kc = (uint32_t)(lane & 15) << 2;
+  const SmallKeys kk = small_keys(lane);
   const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch (<= 64 C)
   const uint32_t stage = kSmallStage + (uint32_t)wave * 1024u * C;
   const uint32_t nb = (a.n + 63) / 64;
@@ -511,9 +538,9 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
   // one chain over dwords [0, n) with per-lane masks (IPv4 options, the
   // direct path, malformed frames)
   auto one_chain = [&](int ihl, auto rd) {
-    uint32_t R = 0;
-    for (int k = 0; k < n; ++k) R = mul32_rep16(R ^ fix_dword(rd(k), k, ihl + 1, ihl + 3), kc);
-    return R;
+    uint32_t P = 0, T = 0;
+    for (int k = 0; k < n; ++k) absorb16(P, T, fix_dword(rd(k), k, ihl + 1, ihl + 3), kk);
+    return P ^ T;
   };
   auto load = [&](uint32_t b, u32x4* Rg) {  // unconditional: clamped chunk index
     const uint8_t* base = a.frames + (uint64_t)min(b, last - 1) * 64u * S;
@@ -537,18 +564,18 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
       lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
       lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
       __asm__ __volatile__("" ::: "memory");
-      uint32_t A = 0, B = 0, Cc = 0, D = 0;
+      uint32_t AP = 0, AT = 0, BP = 0, BT = 0, CP = 0, CT = 0, DP = 0, DT = 0;
       const uint32_t pa = pb, pbb = pb + 4u * q, pc = pb + 8u * q, pd = pb + 12u * q;
       for (int j = 0; j < q; ++j) {
-        A = mul32_rep16(A ^ lds_rd(pa + 4u * j), kc);
-        B = mul32_rep16(B ^ lds_rd(pbb + 4u * j), kc);
-        Cc = mul32_rep16(Cc ^ lds_rd(pc + 4u * j), kc);
-        D = mul32_rep16(D ^ lds_rd(pd + 4u * j), kc);
+        absorb16(AP, AT, lds_rd(pa + 4u * j), kk);
+        absorb16(BP, BT, lds_rd(pbb + 4u * j), kk);
+        absorb16(CP, CT, lds_rd(pc + 4u * j), kk);
+        absorb16(DP, DT, lds_rd(pd + 4u * j), kk);
       }
-      for (int j = q; j < rlen; ++j) D = mul32_rep16(D ^ lds_rd(pd + 4u * j), kc);
-      R = mul_comb(A, kSmallComb) ^ B;
-      R = mul_comb(R, kSmallComb) ^ Cc;
-      R = mul_comb(R, kSmallComb + 4096u) ^ D;
+      for (int j = q; j < rlen; ++j) absorb16(DP, DT, lds_rd(pd + 4u * j), kk);
+      R = mul_comb(AP ^ AT, kSmallComb) ^ BP ^ BT;
+      R = mul_comb(R, kSmallComb) ^ CP ^ CT;
+      R = mul_comb(R, kSmallComb + 4096u) ^ DP ^ DT;
     } else {
       R = one_chain(ihl, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
     }

@@ -87,6 +87,29 @@ def main():
                                   "GiBps": cov / med / 2**30}), flush=True)
             eng.set_lanes(0)
             del d, do, dl, out, ok
+        elif cfg.startswith("u"):
+            # homogeneous frames of payload P ("u256"): the strided kernel and the
+            # ragged kernel (offsets i * stride) on the same buffer, per lane setting
+            pay = int(cfg[1:])
+            flen0 = pay + 44
+            n = min(1 << 24, (2 << 30) // flen0)
+            buf, stride, flen = synth.uniform_frames(n, pay, seed=synth.SEED_CFG2)
+            cov = (flen - 4) * n
+            d = torch.from_numpy(buf).cuda()
+            del buf
+            do = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+            dl = torch.full((n,), flen, dtype=torch.int32, device="cuda")
+            out = torch.zeros(n, dtype=torch.int32, device="cuda")
+            for g in lanes:
+                eng.set_lanes(g)
+                med, _ = timed(lambda: eng.compute_strided_dev(d, stride, flen, n, out, stream=sp),
+                               args.reps, s)
+                med2, _ = timed(lambda: eng.compute_batch_dev(d, do, dl, n, out, stream=sp),
+                                args.reps, s)
+                print(json.dumps({"cfg": cfg, "lanes": g, "n": n, "strided_GiBps": cov / med / 2**30,
+                                  "ragged_GiBps": cov / med2 / 2**30}), flush=True)
+            eng.set_lanes(0)
+            del d, do, dl, out
         print(json.dumps({"cfg": cfg, "wall_s": time.time() - t0}), flush=True)
         torch.cuda.empty_cache()
 
