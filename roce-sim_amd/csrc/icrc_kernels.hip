@@ -192,6 +192,11 @@ __device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
   return b;
 }
 
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
+                                            uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
+                                            int base, uint32_t kc0, uint32_t kc1);
+
 // Fold, combine, check and emit one packet whose first batch is in `b`.
 template <int LOG2G, bool VERIFY>
 __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, Batch<kUnroll>& b,
@@ -246,8 +251,16 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     if (JL < p.jh) fix_chunk5(w, kb, kLut, h0, h2);
     fold_last(A, w, kb, p.n, kc0, kc1);
   }
+  emit_packet<LOG2G, VERIFY>(a, p, A, h0, h2, b.trailer, gl, base, kc0, kc1);
+}
 
-  // ---- packet done: fold the group, check the header, emit ------------------
+// Packet done: fold the group's columns, check the header, emit.
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
+                                            uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
+                                            int base, uint32_t kc0, uint32_t kc1) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
   uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
                               A.P[3] ^ A.T[3], p.r, gl, base);
   const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
@@ -269,7 +282,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   const uint32_t icrc = good ? ~B : 0u;
   if (p.live && gl == 0) {
     if constexpr (VERIFY) {
-      const bool ok = good && b.trailer == icrc;
+      const bool ok = good && trailer == icrc;
       if (good && !ok) st |= kPktIcrcMismatch;
       a.ok_out[p.pkt] = ok ? 1 : 0;
     }
@@ -434,7 +447,7 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
 // and the masks applied in LDS rather than by uniform selects in the loop.
 //
 // LDS: [0, 64 KiB) Mul(32) replicated 16x, [64, 72 KiB) the two combine
-// sets, then kSmallWaves slots of 1024 C bytes.  Replica layout: entry e of
+// sets, then one staging slot of 64 x stride bytes per wave.  Replica layout: entry e of
 // table t, copy c at e * 256 + t * 64 + c * 4 (c = lane & 15).  Lanes l and
 // l + 16 of a ds_read_b32 half-wave share copy c, so they read DIFFERENT
 // tables in each of the four lookups (lane half h = (lane >> 4) & 1 reads
@@ -444,7 +457,9 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
 // (x byte (i ^ h) -> byte 1, the per-lane copy/table offset -> byte 0) with
 // per-lane selector registers; the odd lookups' table offset is folded into
 // their own constant, the upper pair's 128 into the instruction offset.
-constexpr int kSmallWaves = 8;
+// Waves per workgroup: as many 64 x stride slots as the LDS holds, at most
+// kSmallMaxWaves (3 waves per SIMD; the kernel's VGPR budget is 512 / 3).
+constexpr int kSmallMaxWaves = 12;
 constexpr uint32_t kSmallComb = 65536;
 constexpr uint32_t kSmallStage = kSmallComb + 8192;
 
@@ -477,7 +492,7 @@ __device__ __forceinline__ void absorb16(uint32_t& P, uint32_t& T, uint32_t w, c
 }
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
-__global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArgs a) {
+__global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
   const uint32_t S = (uint32_t)a.stride, L = a.len;
   const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
@@ -485,13 +500,13 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
   const int q = n >> 2, rlen = n - 3 * q;        // chain lengths
   {
     const uint32_t* m32 = a.tables + kSmallSet * 1024;
-    for (int i = tid; i < 16384; i += 64 * kSmallWaves) {  // 16 copies of 1024 words
+    for (int i = tid; i < 16384; i += (int)blockDim.x) {  // 16 copies of 1024 words
       const int w = i >> 4, c = i & 15;  // w = t * 256 + e
       lds_wr((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + c * 4), m32[w]);
     }
     const uint32_t* cq = a.tables + (kSmallSet + max(q, 1) - 1) * 1024;
     const uint32_t* cr = a.tables + (kSmallSet + max(rlen, 1) - 1) * 1024;
-    for (int i = tid; i < 1024; i += 64 * kSmallWaves) {
+    for (int i = tid; i < 1024; i += (int)blockDim.x) {
       lds_wr(kSmallComb + 4u * i, cq[i]);
       lds_wr(kSmallComb + 4096u + 4u * i, cr[i]);
     }
@@ -500,7 +515,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
   const int lane = tid & 63, wave = tid >> 6;
   const SmallKeys kk = small_keys(lane);
   const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch (<= 64 C)
-  const uint32_t stage = kSmallStage + (uint32_t)wave * 1024u * C;
+  const uint32_t nw = blockDim.x >> 6;
+  const uint32_t stage = kSmallStage + (uint32_t)wave * 64u * S;
   const uint32_t nb = (a.n + 63) / 64;
   const uint32_t last = nb - 1;  // the batch holding packet n-1: direct path
   const uint32_t per_block = (nb + gridDim.x - 1) / gridDim.x;
@@ -549,7 +565,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
   };
   auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext) {
 #pragma unroll
-    for (int t = 0; t < C; ++t) *(lds_u32x4*)(uintptr_t)(stage + 16u * (uint32_t)(lane + 64 * t)) = Rg[t];
+    for (int t = 0; t < C; ++t)  // chunks past the batch hold a copy of its last one
+      *(lds_u32x4*)(uintptr_t)(stage + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1)) = Rg[t];
     __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
     load(bnext, Rg);  // the registers are free again: prefetch the next batch
     const uint32_t pb = stage + (uint32_t)lane * S;
@@ -583,26 +600,26 @@ __global__ void __launch_bounds__(64 * kSmallWaves, 1) icrc_small_kernel(IcrcArg
     __asm__ __volatile__("" ::: "memory");
   };
 
-  // staged batches [b0 + wave, min(b1, last)) step kSmallWaves; each batch's
+  // staged batches [b0 + wave, min(b1, last)) step nw; each batch's
   // loads are issued two batches ahead (buffers X, Y), right after the batch
   // that used the buffer is staged
   const uint32_t bs_end = min(b1, last);
   if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
     const uint32_t first = b0 + (uint32_t)wave;
-    const int cnt = first < bs_end ? (int)((bs_end - first + kSmallWaves - 1) / kSmallWaves) : 0;
+    const int cnt = first < bs_end ? (int)((bs_end - first + nw - 1) / nw) : 0;
     u32x4 X[C], Y[C];
     load(first, X);
-    load(first + kSmallWaves, Y);
+    load(first + nw, Y);
     uint32_t b = first;
     int i = 0;
-    for (; i + 1 < cnt; i += 2, b += 2 * kSmallWaves) {
-      stage_and_fold(b, X, b + 2 * kSmallWaves);
-      stage_and_fold(b + kSmallWaves, Y, b + 3 * kSmallWaves);
+    for (; i + 1 < cnt; i += 2, b += 2 * nw) {
+      stage_and_fold(b, X, b + 2 * nw);
+      stage_and_fold(b + nw, Y, b + 3 * nw);
     }
-    if (i < cnt) stage_and_fold(b, X, b + 2 * kSmallWaves);
+    if (i < cnt) stage_and_fold(b, X, b + 2 * nw);
   }
   // the last batch, straight from global memory (one wave of the owning block)
-  if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % kSmallWaves) {
+  if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % nw) {
     const uint32_t pkt = last * 64u + (uint32_t)lane;
     const bool live = pkt < a.n;
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
@@ -726,23 +743,25 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   const int C = a.stride <= 64 ? 4 : 8;  // 16-byte loads per lane per batch (4 * stride / 64)
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
   kernel_fn k = select_small(C, verify, outs);
-  const size_t lds = kSmallStage + (size_t)kSmallWaves * 1024u * C;
+  const uint32_t slot = 64u * (uint32_t)a.stride;
+  const uint32_t nw = min((uint32_t)kSmallMaxWaves, (163840u - kSmallStage) / slot);
+  const size_t lds = kSmallStage + (size_t)nw * slot;
   static const hipError_t prep = [] {
     for (int c : {4, 8})
       for (int v = 0; v < 2; ++v)
         for (int o = 0; o < 4; ++o) {
           hipError_t e = hipFuncSetAttribute((const void*)select_small(c, v, o),
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)(kSmallStage + kSmallWaves * 1024u * 8));
+                                             163840);
           if (e != hipSuccess) return e;
         }
     return hipSuccess;
   }();
   if (prep != hipSuccess) return prep;
   const uint64_t nb = (a.n + 63) / 64;
-  uint64_t blocks = (nb + kSmallWaves - 1) / kSmallWaves;
+  uint64_t blocks = (nb + nw - 1) / nw;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kSmallWaves), lds, stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * nw), lds, stream, a);
   return hipGetLastError();
 }
 
