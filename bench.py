@@ -211,13 +211,19 @@ class RaggedVerify:
         self.buf = self.d_frames.cpu().numpy()  # host copy with trailers + corruptions
 
     def step(self, sp):
+        # verdicts only (1 B per packet); the ICRC words came from the compute path
         self.eng.verify_batch_dev(self.d_frames, self.d_offs, self.d_lens, self.n, self.ok,
-                                  self.icrc, stream=sp)
+                                  stream=sp)
 
     def upload(self, h_frames):
         self.d_frames.copy_(h_frames, non_blocking=True)
 
     def results(self):
+        # ICRC words of the frames as they now are (faults included): the
+        # compute path over the same bytes the CPU baseline reads
+        sp = self.torch.cuda.current_stream(self.d_frames.device).cuda_stream
+        self.eng.compute_batch_dev(self.d_frames, self.d_offs, self.d_lens, self.n, self.icrc,
+                                   stream=sp)
         return self.icrc.cpu().numpy().view(np.uint32).copy()
 
     def lanes(self):

@@ -28,21 +28,24 @@ echo "== pmc WRITE_SIZE"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcw_$TAG -o run -- python3 $R/bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmcw_$TAG.log 2>&1
 rc=$?; tail -2 $OUT/pmcw_$TAG.log; echo "pmcw rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R
+# algorithmic bytes and the ceiling kernel's byte count from the bench line itself
+ALG=$(python3 -c "import json; d=json.load(open('$OUT/bench_$TAG.json')); print(d['roofline']['alg_bytes_per_launch'])")
+NP=$(python3 -c "import json; d=json.load(open('$OUT/bench_$TAG.json')); print(d['config']['packets_per_gpu'])")
 if [ "$WL" = seg ]; then
-  N=$(python3 -c "import bench; print(bench.WORKLOADS['seg'][1])")
-  MR=$((N * 4096))
+  MR=$((NP * 4096))
   python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload seg \
-    --packets $N --frame-bytes 4140 --kernel segment_kernel --ceiling stream_copy_kernel \
-    --ceiling-read-bytes $MR --alg-bytes $((MR + N * 4140 + 8 * N)) \
-    --out $OUT/pmc_traffic_${TAG}_seg.json || exit 1
+    --packets $NP --frame-bytes 4140 --kernel segment_kernel --ceiling stream_copy_kernel \
+    --ceiling-read-bytes $MR --alg-bytes $ALG --out $OUT/pmc_traffic_${TAG}_seg.json || exit 1
   KN=segment_kernel
 else
-  python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
-    --packets $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][1])") \
-    --frame-bytes $(python3 -c "import bench; print(bench.WORKLOADS['$WL'][0] + 44)") \
-    --out $OUT/pmc_traffic_${TAG}_$WL.json || exit 1
+  # the STREAM-read kernel reads the whole frame buffer: covered bytes + 4 B per frame
+  BUF=$(python3 -c "import json; d=json.load(open('$OUT/bench_$TAG.json')); c=d['config']; print((c['covered_bytes_per_gpu'] + 4 * c['packets_per_gpu']) // 16 * 16)")
   KN=::icrc_
+  [ "$WL" = cfg3 ] && KN=", true>"  # the verify kernel (the compute launch in setup fills trailers)
+  python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
+    --packets $NP --frame-bytes 0 --ceiling-read-bytes $BUF --alg-bytes $ALG --kernel "$KN" \
+    --out $OUT/pmc_traffic_${TAG}_$WL.json || exit 1
 fi
-python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json $KN > $OUT/prof_summary_$TAG.txt || exit 1
+python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json "$KN" > $OUT/prof_summary_$TAG.txt || exit 1
 cat $OUT/prof_summary_$TAG.txt
 exit 0
