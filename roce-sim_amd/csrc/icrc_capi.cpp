@@ -39,6 +39,10 @@ struct ricrc_ctx {
   size_t mr_cap = 0;
   ricrc_seg_wr* d_wrs = nullptr;
   size_t wr_cap = 0;
+  // small host calls (the per-packet drop-in): one pinned staging block and
+  // its device twin, so a call is one H2D copy, one kernel, one D2H copy
+  uint8_t* h_stage = nullptr;
+  uint8_t* d_stage = nullptr;
 };
 
 namespace {
@@ -146,7 +150,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   a.ok_out = ok;
   a.tables = c->d_tables;
   HIP_TRY(hipSetDevice(c->device));
-  if (!ragged && n > 0 && use_small(c, stride, len))
+  if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0)
     HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
   else
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
@@ -161,6 +165,58 @@ uint32_t mean_len(const uint32_t* lens, uint32_t n) {
   return (uint32_t)(s / n);
 }
 
+// Small host calls (the per-packet drop-in) go through one pinned staging
+// block and its device twin: the caller's frames, offsets and lengths are
+// packed into it ([frames | offsets | lens], then [icrc | status | ok] on the
+// way back), so a call is one H2D copy, one kernel and one D2H copy instead
+// of three copies in and up to three out from pageable memory: 51 -> 25 us
+// per ricrc_compute_one on MI355X.  (Measured and not kept: a zero-copy
+// variant, the kernel reading the mapped host block over PCIe, and polling
+// hipStreamQuery instead of hipStreamSynchronize -- both the same latency;
+// the floor is the launch + copy + synchronise round trip.)
+constexpr size_t kStageBytes = 1u << 20;
+constexpr size_t kStageMaxFrames = 256u << 10;  // larger calls use the device scratch
+size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
+
+int ensure_stage(ricrc_ctx* c) {
+  if (c->h_stage) return RICRC_OK;
+  HIP_TRY(hipHostMalloc((void**)&c->h_stage, kStageBytes, hipHostMallocDefault));
+  if (hipMalloc(&c->d_stage, kStageBytes) != hipSuccess) {
+    (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    return RICRC_ENOMEM;
+  }
+  return RICRC_OK;
+}
+
+int host_ragged_staged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,
+                       const uint64_t* offsets, const uint32_t* lens, uint32_t n,
+                       uint32_t* icrc_out, uint8_t* status_out, uint8_t* ok_out, bool verify) {
+  int rc = ensure_stage(c);
+  if (rc) return rc;
+  const size_t o_offs = up256(frames_bytes), o_lens = o_offs + up256(8ull * n);
+  const size_t in_bytes = o_lens + 4ull * n;
+  const size_t o_icrc = up256(in_bytes), o_st = o_icrc + up256(4ull * n), o_ok = o_st + up256(n);
+  uint8_t* h = c->h_stage;
+  uint8_t* d = c->d_stage;
+  std::memcpy(h, frames, frames_bytes);
+  std::memcpy(h + o_offs, offsets, 8ull * n);
+  std::memcpy(h + o_lens, lens, 4ull * n);
+  HIP_TRY(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
+  rc = launch(c, d, (const uint64_t*)(d + o_offs), (const uint32_t*)(d + o_lens), 0, 0, n,
+              (uint32_t*)(d + o_icrc), d + o_st, verify ? d + o_ok : nullptr, true, verify,
+              ragged_log2g(c, mean_len(lens, n)), c->stream);
+  if (rc) return rc;
+  const size_t out_end = verify ? o_ok + n : o_st + n;
+  HIP_TRY(hipMemcpyAsync(h + o_icrc, d + o_icrc, out_end - o_icrc, hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (icrc_out) std::memcpy(icrc_out, h + o_icrc, 4ull * n);
+  if (status_out) std::memcpy(status_out, h + o_st, n);
+  if (verify) std::memcpy(ok_out, h + o_ok, n);
+  return RICRC_OK;
+}
+
 int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const uint64_t* offsets,
                 const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,
                 uint8_t* ok_out, bool verify) {
@@ -171,6 +227,9 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
   for (uint32_t i = 0; i < n; ++i)
     if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
+  if (frames_bytes <= kStageMaxFrames && 32ull * n + 1536 <= kStageBytes - up256(frames_bytes))
+    return host_ragged_staged(c, frames, frames_bytes, offsets, lens, n, icrc_out, status_out,
+                              ok_out, verify);
   int rc = ensure_frames(c, frames_bytes);
   if (rc) return rc;
   rc = ensure_pkts(c, n);
@@ -321,6 +380,8 @@ void ricrc_ctx_destroy(ricrc_ctx* c) {
   (void)hipFree(c->d_ok);
   (void)hipFree(c->d_mr);
   (void)hipFree(c->d_wrs);
+  (void)hipFree(c->d_stage);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

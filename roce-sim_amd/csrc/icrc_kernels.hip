@@ -76,7 +76,7 @@ __device__ __forceinline__ Pkt describe(const uint8_t* frames, uint32_t pkt, boo
   p.L = L;
   p.pkt = pkt;
   p.live = live;
-  p.dead = !live || L < 44 || (L & 3u) || L > 65535u;
+  p.dead = !live || L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)p.fp & 3u);
   p.S = (int)(((uintptr_t)p.fp >> 2) & (DPI - 1));
   p.ab = p.fp - 4 * p.S;
   p.n = p.dead ? 1 : (int)((L - 4) >> 2);
@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
       if (i < cnt) {
         const uint32_t L = a.lens[w0 + i];
         const uint64_t off = a.offsets[w0 + i];
-        if (!(L < 44 || (L & 3u) || L > 65535u)) {
+        if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
           const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
           key = min(NB - 1, (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
         }

@@ -1,0 +1,55 @@
+"""Per-call latency of the host-buffer entry points (the per-packet drop-in
+path of BTH.compute_icrc, src/roce.py:192): ricrc_compute_one and small
+ricrc_compute_batch / ricrc_verify_batch calls, synchronous H2D + kernel + D2H.
+
+usage: python scripts/latency.py [--reps 300]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "roce-sim_amd"))
+from roce_icrc import IcrcEngine, synth  # noqa: E402
+
+
+def med_us(fn, reps):
+    for _ in range(20):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts) * 1e6), float(np.percentile(ts, 99) * 1e6)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=300)
+    a = ap.parse_args()
+    eng = IcrcEngine(0)
+    for pay in (64, 1024, 4096):
+        buf, stride, flen = synth.uniform_frames(1, pay)
+        frame = bytes(buf[:flen])
+        med, p99 = med_us(lambda: eng.compute_one(frame), a.reps)
+        print(json.dumps({"call": "compute_one", "frame_bytes": flen, "median_us": round(med, 2),
+                          "p99_us": round(p99, 2)}), flush=True)
+    for n in (16, 256, 4096):
+        buf, offs, lens = synth.mixed_mtu_frames(n, seed=3)
+        med, p99 = med_us(lambda: eng.compute_batch(buf, offs, lens), max(20, a.reps // 4))
+        cov = synth.covered_bytes(lens)
+        print(json.dumps({"call": "compute_batch", "n": n, "median_us": round(med, 2),
+                          "p99_us": round(p99, 2), "GiBps": round(cov / med / 1e-6 / 2**30, 3)}),
+              flush=True)
+        med, p99 = med_us(lambda: eng.verify_batch(buf, offs, lens), max(20, a.reps // 4))
+        print(json.dumps({"call": "verify_batch", "n": n, "median_us": round(med, 2),
+                          "p99_us": round(p99, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

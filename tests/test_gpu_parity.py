@@ -192,6 +192,29 @@ def test_unaligned_offsets(engine):
     engine.set_lanes(0)
 
 
+def test_misaligned_frame_is_flagged(engine):
+    """A frame whose start is not 4-byte aligned is not read: ICRC 0 and
+    PKT_BAD_LEN (the kernels walk dword-aligned chunks); its neighbours are
+    unaffected, on the staged small-call path and on a large batch."""
+    good = o.build_frame("1.2.3.4", "5.6.7.8", 9, dict(opcode=0x04, psn=7),
+                         payload=bytes(range(256)))
+    for reps in (1, 3000):  # 3000 frames: past the pinned staging block
+        buf = np.zeros((len(good) + 8) * (reps + 1) + 8, np.uint8)
+        offs, lens = [], []
+        pos = 0
+        for i in range(reps):
+            buf[pos:pos + len(good)] = np.frombuffer(good, np.uint8)
+            offs.append(pos)
+            pos += len(good) + 4
+        odd = pos + 2
+        buf[odd:odd + len(good)] = np.frombuffer(good, np.uint8)
+        offs.append(odd)
+        lens = np.full(reps + 1, len(good), np.uint32)
+        got, st = engine.compute_batch(buf, np.array(offs, np.uint64), lens)
+        assert (got[:-1] == o.icrc_of_frame(good)).all() and (st[:-1] == 0).all()
+        assert got[-1] == 0 and st[-1] & PKT_BAD_LEN
+
+
 def test_mask_invariance_and_sensitivity(engine):
     base = o.build_frame("10.9.8.7", "10.6.5.4", 17, dict(opcode=0x0A, psn=99, dqpn=0x42),
                          ext=o.reth_bytes(1, 2, 3), payload=bytes(range(200)))
