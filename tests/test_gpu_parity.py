@@ -192,6 +192,35 @@ def test_unaligned_offsets(engine):
     engine.set_lanes(0)
 
 
+def test_maximum_length_frames(engine):
+    """IPv4's largest frame that is a multiple of 4 (65532 B: 16383 dwords, 2047
+    lane-group iterations at G = 8) between small ones, ragged and strided,
+    compute and verify; 65536 B exceeds the IPv4 total length and is flagged."""
+    rng = np.random.default_rng(65532)
+    big = o.build_frame("10.0.0.1", "10.0.0.2", 5, dict(opcode=0x07, psn=1),
+                        payload=rng.integers(0, 256, 65532 - 44, dtype=np.uint8).tobytes())
+    assert len(big) == 65532
+    small = o.build_frame("10.0.0.1", "10.0.0.2", 5, dict(opcode=0x07, psn=2), payload=b"\1" * 64)
+    over = bytearray(big + b"\0\0\0\0")  # 65536 B: no valid IPv4 total length
+    frames = [small, big, small, big, bytes(over), small]
+    buf, offs, lens = _pack(frames)
+    want = [o.icrc_of_frame(f) for f in frames[:4]] + [0, o.icrc_of_frame(small)]
+    for lanes in (0, 8, 64):
+        engine.set_lanes(lanes)
+        got, st = engine.compute_batch(buf, offs, lens)
+        np.testing.assert_array_equal(got, want)
+        assert st[4] & PKT_BAD_LEN and (np.delete(st, 4) == 0).all()
+        for i in range(4):
+            e = int(offs[i] + lens[i])
+            buf[e - 4:e] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+        ok, _, _ = engine.verify_batch(buf, offs, lens)
+        assert ok[:4].all() and not ok[4]
+        sbuf = np.frombuffer(big * 3, np.uint8).copy()
+        got, st = engine.compute_strided(sbuf, len(big), len(big), 3)
+        assert (got == want[1]).all() and (st == 0).all()
+    engine.set_lanes(0)
+
+
 def test_misaligned_frame_is_flagged(engine):
     """A frame whose start is not 4-byte aligned is not read: ICRC 0 and
     PKT_BAD_LEN (the kernels walk dword-aligned chunks); its neighbours are
