@@ -12,12 +12,7 @@ namespace ricrc {
 constexpr int kMaxLog2G = 6;
 constexpr int kNumMainSets = kMaxLog2G + 1;
 constexpr int kNumCombSets = kMaxLog2G + 1;
-// ... then the sets Mul(32 m), m = 1 .. kSmallMaxDwords, for the
-// lane-per-packet kernel of small frames: Mul(32) is its per-dword step, the
-// others combine its independent chains (set kSmallSet + m - 1).
-constexpr int kSmallMaxDwords = 31;  // covered dwords of a frame of <= 128 bytes
-constexpr int kSmallSet = kNumMainSets + kNumCombSets;
-constexpr int kTableWords = (kNumMainSets + kNumCombSets + kSmallMaxDwords) * 1024;
+constexpr int kTableWords = (kNumMainSets + kNumCombSets) * 1024;
 
 struct IcrcArgs {
   const uint8_t* frames;

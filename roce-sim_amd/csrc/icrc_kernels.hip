@@ -435,19 +435,22 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
 // consecutive packets: their 64 x stride bytes arrive with fully coalesced
 // 16-byte loads (issued two batches ahead, held in registers), go to the
 // wave's LDS staging slot, each lane patches its frame's masked dwords and
-// seed in place, and folds the frame from LDS.  The n covered dwords form
-// four independent chains (lengths q, q, q, n - 3q; r <- Mul(32)(r ^ w) each)
-// joined by Horner steps with Mul(32 q) and Mul(32 (n - 3q)).  The batch
-// holding the last packet reads its frames straight from global memory (no
-// 16-byte over-read past the buffer) in one chain.
+// seed in place, and folds the frame from LDS as four interleaved chains:
+// chain c takes the dwords k = 4 j + c - pad (pad = 4 ns - n zero dwords in
+// front, ns = ceil(n / 4) steps), (P, T) <- Mul(128)(P ^ T ^ w_k), and the
+// packet register is R = sum_c Mul(-32 c)(chain c) -- three Horner steps with
+// Mul(-32).  The four dwords of a step are consecutive in LDS, read with
+// immediate offsets from one base (ds_read2_b32 pairs), and the joins do not
+// depend on the frame length.  The batch holding the last packet reads its
+// frames straight from global memory (no 16-byte over-read past the buffer).
 //
 // Nothing between a batch's loads and their use may be predicated or fenced:
 // the compiler would then drain every load in flight (vmcnt(0)), including
-// the prefetch.  Hence unconditional LDS writes into a 64 x 16 x C-byte slot
-// and the masks applied in LDS rather than by uniform selects in the loop.
+// the prefetch.  Hence unconditional LDS writes into the slot and the masks
+// applied in LDS rather than by uniform selects in the loop.
 //
-// LDS: [0, 64 KiB) Mul(32) replicated 16x, [64, 72 KiB) the two combine
-// sets, then one staging slot of 64 x stride bytes per wave.  Replica layout: entry e of
+// LDS: [0, 64 KiB) Mul(128) replicated 16x, [64, 68 KiB) Mul(-32), then one
+// staging slot of 64 x stride bytes per wave.  Replica layout: entry e of
 // table t, copy c at e * 256 + t * 64 + c * 4 (c = lane & 15).  Lanes l and
 // l + 16 of a ds_read_b32 half-wave share copy c, so they read DIFFERENT
 // tables in each of the four lookups (lane half h = (lane >> 4) & 1 reads
@@ -457,11 +460,10 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
 // (x byte (i ^ h) -> byte 1, the per-lane copy/table offset -> byte 0) with
 // per-lane selector registers; the odd lookups' table offset is folded into
 // their own constant, the upper pair's 128 into the instruction offset.
-// Waves per workgroup: as many 64 x stride slots as the LDS holds, at most
-// kSmallMaxWaves (3 waves per SIMD; the kernel's VGPR budget is 512 / 3).
 constexpr int kSmallMaxWaves = 12;
 constexpr uint32_t kSmallComb = 65536;
-constexpr uint32_t kSmallStage = kSmallComb + 8192;
+constexpr uint32_t kSmallStage = kSmallComb + 4096;
+constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + 3) / 4;  // ns <= 8
 
 struct SmallKeys {
   uint32_t ke, ko;              // byte 0: c * 4 + h * 64, c * 4 + (1 - h) * 64
@@ -480,7 +482,7 @@ __device__ __forceinline__ SmallKeys small_keys(int lane) {
   return k;
 }
 
-// (P, T) <- Mul(32)(P ^ T ^ w) from the 16x set (P = three lookups, T = the fourth)
+// (P, T) <- Mul(128)(P ^ T ^ w) from the 16x set (P = three lookups, T = the fourth)
 __device__ __forceinline__ void absorb16(uint32_t& P, uint32_t& T, uint32_t w, const SmallKeys& k) {
   const uint32_t x = xor3(P, T, w);
   const uint32_t a0 = __builtin_amdgcn_perm(x, k.ke, k.s0);
@@ -497,19 +499,15 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   const uint32_t S = (uint32_t)a.stride, L = a.len;
   const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
   const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
-  const int q = n >> 2, rlen = n - 3 * q;        // chain lengths
+  const int ns = (n + 3) >> 2, pad = 4 * ns - n;  // steps, zero dwords in front
   {
-    const uint32_t* m32 = a.tables + kSmallSet * 1024;
+    const uint32_t* m128 = a.tables;  // main set 0: Mul(128)
     for (int i = tid; i < 16384; i += (int)blockDim.x) {  // 16 copies of 1024 words
       const int w = i >> 4, c = i & 15;  // w = t * 256 + e
-      lds_wr((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + c * 4), m32[w]);
+      lds_wr((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + c * 4), m128[w]);
     }
-    const uint32_t* cq = a.tables + (kSmallSet + max(q, 1) - 1) * 1024;
-    const uint32_t* cr = a.tables + (kSmallSet + max(rlen, 1) - 1) * 1024;
-    for (int i = tid; i < 1024; i += (int)blockDim.x) {
-      lds_wr(kSmallComb + 4u * i, cq[i]);
-      lds_wr(kSmallComb + 4096u + 4u * i, cr[i]);
-    }
+    const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
+    for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallComb + 4u * i, cm32[i]);
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
@@ -547,16 +545,37 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
         if (good && !ok) st |= kPktIcrcMismatch;
         a.ok_out[pkt] = ok ? 1 : 0;
       }
+#ifdef RICRC_SMALL_STORE_RING  // diagnostic build only: outputs wrap in a ring of that many dwords
+      if constexpr ((OUTS & 1) != 0) a.icrc_out[pkt & (RICRC_SMALL_STORE_RING - 1u)] = icrc;
+#else
       if constexpr ((OUTS & 1) != 0) a.icrc_out[pkt] = icrc;
+#endif
       if constexpr ((OUTS & 2) != 0) a.status_out[pkt] = (uint8_t)st;
     }
   };
-  // one chain over dwords [0, n) with per-lane masks (IPv4 options, the
-  // direct path, malformed frames)
-  auto one_chain = [&](int ihl, auto rd) {
-    uint32_t P = 0, T = 0;
-    for (int k = 0; k < n; ++k) absorb16(P, T, fix_dword(rd(k), k, ihl + 1, ihl + 3), kk);
-    return P ^ T;
+  // the four chains over dwords [0, n); rd(k, kp) returns dword k >= 0
+  // (kp = k + pad, a compile-time index into the padded frame) ready to
+  // absorb; dwords k < 0 are the zero pad
+  auto fold4 = [&](auto rd) {
+    uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kSmallMaxSteps; ++j) {
+      if (j < ns) {  // uniform
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int k = 4 * j + c - pad;
+          const uint32_t w = rd(k < 0 ? 0 : k, 4 * j + c);  // (never read before the frame)
+          absorb16(P[c], T[c], (j == 0 && k < 0) ? 0u : w, kk);
+        }
+      }
+    }
+    uint32_t R = mul_comb(P[3] ^ T[3], kSmallComb) ^ P[2] ^ T[2];
+    R = mul_comb(R, kSmallComb) ^ P[1] ^ T[1];
+    return mul_comb(R, kSmallComb) ^ P[0] ^ T[0];
+  };
+  // per-dword masks (IPv4 options, the direct path, malformed frames)
+  auto fold4_masked = [&](int ihl, auto src) {
+    return fold4([&](int k, int) { return fix_dword(src(k), k, ihl + 1, ihl + 3); });
   };
   auto load = [&](uint32_t b, u32x4* Rg) {  // unconditional: clamped chunk index
     const uint8_t* base = a.frames + (uint64_t)min(b, last - 1) * 64u * S;
@@ -564,6 +583,19 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
   };
   auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext) {
+#ifdef RICRC_SMALL_ABLATE_STAGE  // diagnostic build only: loads and output stores, no LDS, no fold
+    {
+      u32x4 acc = Rg[0];
+#pragma unroll
+      for (int t = 1; t < C; ++t) acc ^= Rg[t];
+      load(bnext, Rg);
+#ifdef RICRC_SMALL_ABLATE_STORE  // ... and no output stores
+      if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u)
+#endif
+        emit(b * 64u + (uint32_t)lane, true, 0u, acc.x ^ acc.y ^ acc.z ^ acc.w, 0u);
+      return;
+    }
+#endif
 #pragma unroll
     for (int t = 0; t < C; ++t)  // chunks past the batch hold a copy of its last one
       *(lds_u32x4*)(uintptr_t)(stage + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1)) = Rg[t];
@@ -581,20 +613,14 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
       lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
       __asm__ __volatile__("" ::: "memory");
-      uint32_t AP = 0, AT = 0, BP = 0, BT = 0, CP = 0, CT = 0, DP = 0, DT = 0;
-      const uint32_t pa = pb, pbb = pb + 4u * q, pc = pb + 8u * q, pd = pb + 12u * q;
-      for (int j = 0; j < q; ++j) {
-        absorb16(AP, AT, lds_rd(pa + 4u * j), kk);
-        absorb16(BP, BT, lds_rd(pbb + 4u * j), kk);
-        absorb16(CP, CT, lds_rd(pc + 4u * j), kk);
-        absorb16(DP, DT, lds_rd(pd + 4u * j), kk);
-      }
-      for (int j = q; j < rlen; ++j) absorb16(DP, DT, lds_rd(pd + 4u * j), kk);
-      R = mul_comb(AP ^ AT, kSmallComb) ^ BP ^ BT;
-      R = mul_comb(R, kSmallComb) ^ CP ^ CT;
-      R = mul_comb(R, kSmallComb + 4096u) ^ DP ^ DT;
+      const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
+#ifdef RICRC_SMALL_ABLATE_FOLD  // diagnostic build only: staging kept, fold removed
+      R = lds_rd(pz + 16u) ^ lds_rd(pz + 60u);
+#else
+      R = fold4([&](int, int kp) { return lds_rd(pz + 4u * (uint32_t)kp); });
+#endif
     } else {
-      R = one_chain(ihl, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
+      R = fold4_masked(ihl, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
     }
     emit(b * 64u + (uint32_t)lane, true, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u);
     __asm__ __volatile__("" ::: "memory");
@@ -602,7 +628,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
 
   // staged batches [b0 + wave, min(b1, last)) step nw; each batch's
   // loads are issued two batches ahead (buffers X, Y), right after the batch
-  // that used the buffer is staged
+  // that used the buffer is staged (a third buffer measured no faster)
   const uint32_t bs_end = min(b1, last);
   if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
     const uint32_t first = b0 + (uint32_t)wave;
@@ -625,7 +651,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
     int ihl;
     const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
-    const uint32_t R = one_chain(ihl, [&](int k) { return ldg32(f + 4 * k); });
+    const uint32_t R = fold4_masked(ihl, [&](int k) { return ldg32(f + 4 * k); });
     emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
   }
 }
@@ -693,7 +719,6 @@ void build_table_image(uint32_t* out) {
   uint32_t* comb = out + kNumMainSets * 1024;
   table_set(-32, comb);
   for (int l = 0; l < kMaxLog2G; ++l) table_set(-(128ll << l), comb + (1 + l) * 1024);
-  for (int m = 1; m <= kSmallMaxDwords; ++m) table_set(32ll * m, out + (kSmallSet + m - 1) * 1024);
 }
 
 hipError_t prepare_kernels() {
