@@ -156,19 +156,19 @@ __device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n,
 }
 
 // LDS staging of the folding tables (every kernel, once per workgroup).
-template <int LOG2G>
+template <int LOG2G, int THREADS = 1024>
 __device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
   constexpr int NCOMB = 1 + LOG2G;
   const uint32_t* gm = tables + LOG2G * 1024;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int i = tid + r * 1024;  // 8192 16-byte quads
+  for (int r = 0; r < 8192 / THREADS; ++r) {
+    const int i = tid + r * THREADS;  // 8192 16-byte quads
     const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
     lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16),
             gm[tab * 256 + e]);
   }
   const uint32_t* gc = tables + kNumMainSets * 1024;
-  for (int i = tid; i < NCOMB * 1024; i += 1024) lds_wr(kLdsMain + 4u * i, gc[i]);
+  for (int i = tid; i < NCOMB * 1024; i += THREADS) lds_wr(kLdsMain + 4u * i, gc[i]);
   if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
     const int k = tid - 3;
     const uint32_t lut = kLdsMain + 4096u * NCOMB;

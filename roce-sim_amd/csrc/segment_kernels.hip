@@ -47,7 +47,15 @@ __device__ __forceinline__ u32x4 ldmr(const uint8_t* p) {
 #endif
 }
 
-constexpr int kSegUnroll = 4;          // body iterations (16-byte MR loads per lane) in flight
+#ifndef RICRC_SEG_UNROLL
+#define RICRC_SEG_UNROLL 4
+#endif
+#ifndef RICRC_SEG_THREADS
+#define RICRC_SEG_THREADS 512  // 8 waves x ~200 VGPRs: no spills (16 waves spill ~20 VGPRs)
+#endif
+constexpr int kSegUnroll = RICRC_SEG_UNROLL;  // body iterations (16-byte MR loads per lane) in flight
+constexpr int kSegThreads = RICRC_SEG_THREADS;  // one workgroup per CU (the tables fill the LDS)
+constexpr int kSegWaves = kSegThreads / 64;
 constexpr uint32_t kRocePort = 4791;   // src/roce_enum.py ROCE_PORT
 constexpr uint32_t kAckValue = 31;     // CREDIT_CNT_INVALID, src/roce_enum.py:8
 constexpr uint32_t kPktSegBad = 0x20;  // RICRC_PKT_SEG_BAD
@@ -265,13 +273,13 @@ __device__ __forceinline__ void csum_add(uint64_t& acc, const u32x4& w) {
 }
 
 template <int LOG2G>
-__global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
+__global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   constexpr int PPW = 64 / G;
   constexpr int U = kSegUnroll;
   const int tid = threadIdx.x;
-  stage_tables<LOG2G>(a.tables, tid);
+  stage_tables<LOG2G, kSegThreads>(a.tables, tid);
   __syncthreads();
 
   const int lane = tid & 63;
@@ -289,7 +297,7 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
   const uint32_t set_begin = blockIdx.x * per_block;
   const uint32_t set_end = min(nsets, set_begin + per_block);
 
-  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kSegWaves) {
     const uint32_t pkt = set * PPW + grp;
     uint32_t status;
     const Seg s = describe_seg(a, pkt, pkt < a.npkts, status);
@@ -315,9 +323,15 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
     Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     uint64_t acc = 0;
 
-    // Chunks holding the UDP checksum (dword 6) or the ICRC slot are stored
-    // with zeros there; the same lane rewrites those bytes once the group has
-    // combined (a lane's stores to one address stay in program order).
+    // The frame's first and last iterations (one 128-byte line each at G = 8:
+    // the slot is 256-byte aligned) are kept in registers and stored once the
+    // group has combined, with the UDP checksum (dword 6) and the ICRC (dword
+    // T-1) in place: every line of a frame is written whole, by one wave
+    // instruction per iteration.  (Rewriting the 2 + 4 bytes into lines already
+    // streamed out measured 4-6 % slower than not writing them at all; holding
+    // only the two 16-byte chunks, so those lines went out in two parts, was
+    // slower still.)
+    u32x4 hold0 = {0, 0, 0, 0}, holdL = {0, 0, 0, 0};
     auto edge = [&](int j, const u32x4& v, auto head) {
       const int idx0 = DPI * j + 4 * gl;
       if (idx0 >= s.T) return;
@@ -329,7 +343,12 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
       if (idx0 + 2 < 5) cs.z = 0;
       if (idx0 + 3 < 5) cs.w = 0;
       csum_add(acc, cs);
-      __builtin_nontemporal_store(w, (u32x4*)(s.dst + 4 * idx0));
+      if (j == 0)
+        hold0 = w;
+      else if (j == Jw - 1)
+        holdL = w;
+      else
+        __builtin_nontemporal_store(w, (u32x4*)(s.dst + 4 * idx0));
       if (j < J) {  // CRC: masked header dwords, seed, columns past the end skipped
         w.x = fix_dword(w.x, idx0 + 0, 6, 8);
         w.y = fix_dword(w.y, idx0 + 1, 6, 8);
@@ -430,11 +449,18 @@ __global__ void __launch_bounds__(1024, 1) segment_kernel(SegArgs a) {
       t = fold16(fold16(t));
       uint32_t c = (~t) & 0xFFFFu;
       if (c == 0) c = 0xFFFFu;  // UDP: a computed 0 goes out as 0xFFFF
-      if (gl == (4 >> 2)) {  // the lane that stored dword 6 (iteration 0, G >= 2)
-        const uint16_t cs = (uint16_t)c;
-        *(uint16_t*)(s.dst + 26) = cs;
+      if (gl == (4 >> 2)) hold0.z = (hold0.z & 0xFFFFu) | (c << 16);  // dword 6 (G >= 2)
+      const int jl = Jw - 1, idxL = DPI * jl + 4 * gl;
+      if (idxL <= t_last && t_last < idxL + 4) {  // the lane holding the ICRC slot
+        u32x4& h = jl == 0 ? hold0 : holdL;
+        const int t = t_last - idxL;
+        h.x = t == 0 ? icrc : h.x;
+        h.y = t == 1 ? icrc : h.y;
+        h.z = t == 2 ? icrc : h.z;
+        h.w = t == 3 ? icrc : h.w;
       }
-      if (gl == ((t_last & (DPI - 1)) >> 2)) *(uint32_t*)(s.dst + 4 * t_last) = icrc;
+      if (4 * gl < s.T) __builtin_nontemporal_store(hold0, (u32x4*)(s.dst + 16 * gl));
+      if (jl > 0 && idxL < s.T) __builtin_nontemporal_store(holdL, (u32x4*)(s.dst + 4 * idxL));
     }
     if (pkt < a.npkts && gl == 0) {
       a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;
@@ -508,10 +534,10 @@ hipError_t launch_segment(const SegArgs& a, int log2g, int num_cus, hipStream_t 
   }
   const uint32_t ppw = 64u >> log2g;
   const uint64_t nsets = (a.npkts + ppw - 1) / ppw;
-  uint64_t blocks = (nsets + 15) / 16;
+  uint64_t blocks = (nsets + kSegWaves - 1) / kSegWaves;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), seg_lds_bytes(log2g), stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kSegThreads), seg_lds_bytes(log2g), stream, a);
   return hipGetLastError();
 }
 
