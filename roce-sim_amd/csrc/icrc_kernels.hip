@@ -47,6 +47,13 @@ namespace ricrc {
 namespace {
 
 
+// Lane-group kernels: one workgroup per CU (the replicated tables fill the LDS).
+#ifndef RICRC_THREADS
+#define RICRC_THREADS 1024
+#endif
+constexpr int kIcrcThreads = RICRC_THREADS;
+constexpr int kIcrcWaves = kIcrcThreads / 64;
+
 constexpr uint32_t kPktBadLen = 0x01, kPktNotIpv4 = 0x02, kPktNotUdp = 0x04,
                    kPktLenMismatch = 0x08, kPktIcrcMismatch = 0x10,
                    kPktFatal = kPktBadLen | kPktNotIpv4 | kPktNotUdp;
@@ -293,11 +300,11 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
 
 // Fixed-size frames at frames + i * stride.
 template <int LOG2G, bool VERIFY>
-__global__ void __launch_bounds__(1024, 1) icrc_strided_kernel(IcrcArgs a) {
+__global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;  // packets per wave step
   const int tid = threadIdx.x;
-  stage_tables<LOG2G>(a.tables, tid);
+  stage_tables<LOG2G, kIcrcThreads>(a.tables, tid);
   __syncthreads();
 
   const int lane = tid & 63;
@@ -321,7 +328,7 @@ __global__ void __launch_bounds__(1024, 1) icrc_strided_kernel(IcrcArgs a) {
   };
   // (issuing the next set's first batch before finishing this one was
   // measured: no gain at 4 KiB or 108-B frames, and register spills)
-  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += 16u) {
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kIcrcWaves) {
     const Pkt p = make(set);
     Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
     finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kc0, kc1);
@@ -346,7 +353,7 @@ struct RaggedLds {
 };
 
 template <int LOG2G, bool VERIFY>
-__global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
+__global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;
   constexpr int DPI = 4 * G;
@@ -354,7 +361,7 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
   constexpr int W = LD::kWindow;
   constexpr int NB = LD::kBuckets;
   const int tid = threadIdx.x;
-  stage_tables<LOG2G>(a.tables, tid);
+  stage_tables<LOG2G, kIcrcThreads>(a.tables, tid);
 
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
@@ -373,10 +380,11 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
     if (tid < NB) hist[tid] = 0;
     __syncthreads();
     // iteration count of every packet of the window -> bucket
-    int keys[(W + 1023) / 1024];
+    constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
+    int keys[KR];
 #pragma unroll
-    for (int r = 0; r < (W + 1023) / 1024; ++r) {
-      const int i = tid + r * 1024;
+    for (int r = 0; r < KR; ++r) {
+      const int i = tid + r * kIcrcThreads;
       int key = 0;
       if (i < cnt) {
         const uint32_t L = a.lens[w0 + i];
@@ -404,8 +412,8 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < (W + 1023) / 1024; ++r) {
-      const int i = tid + r * 1024;
+    for (int r = 0; r < KR; ++r) {
+      const int i = tid + r * kIcrcThreads;
       if (i < cnt) perm[atomicAdd((uint32_t*)&hist[keys[r]], 1u)] = (uint16_t)i;
     }
     __syncthreads();
@@ -417,7 +425,7 @@ __global__ void __launch_bounds__(1024, 1) icrc_ragged_kernel(IcrcArgs a) {
       return describe<DPI>(a.frames, pkt, live, live ? a.offsets[pkt] : 0,
                            live ? a.lens[pkt] : 0);
     };
-    for (int set = tid >> 6; set < nsets; set += 16) {
+    for (int set = tid >> 6; set < nsets; set += kIcrcWaves) {
       const Pkt p = make(set);
       Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
       finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kc0, kc1);
@@ -740,10 +748,10 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   if (!k) return hipErrorInvalidValue;
   const uint32_t ppw = 64u >> log2g;
   const uint64_t nsets = (a.n + ppw - 1) / ppw;
-  uint64_t blocks = (nsets + 15) / 16;
+  uint64_t blocks = (nsets + kIcrcWaves - 1) / kIcrcWaves;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), lds_bytes(log2g, ragged), stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kIcrcThreads), lds_bytes(log2g, ragged), stream, a);
   return hipGetLastError();
 }
 
