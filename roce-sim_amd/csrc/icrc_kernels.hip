@@ -348,8 +348,11 @@ struct RaggedLds {
   static constexpr uint32_t kHist = kBase;               // kBuckets x u32 counts / cursors
   static constexpr uint32_t kPerm = kBase + 4 * kBuckets;  // window x u16 local indices
   static constexpr int kAvail = (int)(163840u - kPerm);
-  static constexpr int kWindow = (kAvail / 2 >= 4096) ? 4096 : (kAvail / 2) / 64 * 64;
-  static constexpr uint32_t kBytes = kPerm + 2 * kWindow;
+  // sorted descriptors: u16 local index, u32 offset / 4, u16 length (8 B)
+  static constexpr int kWindow = (kAvail / 8 >= 4096) ? 4096 : (kAvail / 8) / 64 * 64;
+  static constexpr uint32_t kRoff = kPerm + 2 * kWindow;
+  static constexpr uint32_t kRlen = kRoff + 4 * kWindow;
+  static constexpr uint32_t kBytes = kRlen + 2 * kWindow;
 };
 
 template <int LOG2G, bool VERIFY>
@@ -374,6 +377,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   typedef __attribute__((address_space(3))) uint16_t lds_u16;
   lds_u32* hist = (lds_u32*)(uintptr_t)LD::kHist;
   lds_u16* perm = (lds_u16*)(uintptr_t)LD::kPerm;
+  lds_u32* roff = (lds_u32*)(uintptr_t)LD::kRoff;
+  lds_u16* rlen = (lds_u16*)(uintptr_t)LD::kRlen;
+  constexpr uint32_t kNoOff = 0xFFFFFFFFu;  // offset not representable: read it from HBM
 
   for (uint32_t w0 = p0; w0 < p1; w0 += W) {
     const int cnt = (int)min((uint32_t)W, p1 - w0);
@@ -382,13 +388,18 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
     // iteration count of every packet of the window -> bucket
     constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
     int keys[KR];
+    uint32_t offw[KR], lw[KR];
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int i = tid + r * kIcrcThreads;
       int key = 0;
+      offw[r] = kNoOff;
+      lw[r] = 0;
       if (i < cnt) {
         const uint32_t L = a.lens[w0 + i];
         const uint64_t off = a.offsets[w0 + i];
+        if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
+        lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
         if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
           const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
           key = min(NB - 1, (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
@@ -414,16 +425,22 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int i = tid + r * kIcrcThreads;
-      if (i < cnt) perm[atomicAdd((uint32_t*)&hist[keys[r]], 1u)] = (uint16_t)i;
+      if (i < cnt) {
+        const uint32_t pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
+        perm[pos] = (uint16_t)i;
+        roff[pos] = offw[r];
+        rlen[pos] = (uint16_t)lw[r];
+      }
     }
     __syncthreads();
     const int nsets = (cnt + PPW - 1) / PPW;
     auto make = [&](int set) {
       const int idx = set * PPW + grp;
       const bool live = set < nsets && idx < cnt;
-      const uint32_t pkt = live ? w0 + perm[idx] : 0;
-      return describe<DPI>(a.frames, pkt, live, live ? a.offsets[pkt] : 0,
-                           live ? a.lens[pkt] : 0);
+      const int ix = live ? idx : 0;
+      const uint32_t pkt = w0 + perm[ix], ow = roff[ix];
+      const uint64_t off = ow != kNoOff ? (uint64_t)ow << 2 : a.offsets[pkt];
+      return describe<DPI>(a.frames, pkt, live, live ? off : 0, live ? (uint32_t)rlen[ix] : 0);
     };
     for (int set = tid >> 6; set < nsets; set += kIcrcWaves) {
       const Pkt p = make(set);
