@@ -321,3 +321,57 @@ def test_full_size_cfg2_bit_exact(engine):
     del d
     want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
     np.testing.assert_array_equal(got, want)
+
+
+def test_full_size_cfg3_ragged_bit_exact(engine):
+    """BASELINE config 3 at full size (2^20 mixed-MTU frames, several sort
+    windows per workgroup): every ICRC word and verdict against the C oracle,
+    packed in memory order and with the descriptors shuffled (frames in
+    arbitrary order, so the block-local sort sees scattered offsets)."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 20
+    buf, offs, lens = synth.mixed_mtu_frames(n)
+    want, _ = oracle_batch(buf, offsets=offs, lens=lens)
+    d = torch.from_numpy(buf).cuda()
+    s = torch.cuda.current_stream()
+    perm = np.random.default_rng(3).permutation(n)
+    for o, l in ((offs, lens), (offs[perm], lens[perm])):
+        do = torch.from_numpy(np.ascontiguousarray(o).view(np.int64)).cuda()
+        dl = torch.from_numpy(np.ascontiguousarray(l).view(np.int32)).cuda()
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        engine.compute_batch_dev(d, do, dl, n, out, stream=s.cuda_stream)
+        s.synchronize()
+        exp = want if o is offs else want[perm]
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+    # trailers filled with the words: every verdict passes, then one byte of
+    # every 997th frame flipped (past its 40-byte header): those fail
+    trail = offs.astype(np.int64) + lens.astype(np.int64) - 4
+    idx = (trail[:, None] + np.arange(4)[None, :]).reshape(-1)
+    buf[idx] = want.view(np.uint8)
+    bad = np.arange(0, n, 997)
+    buf[offs[bad].astype(np.int64) + 44] ^= 0x40
+    d = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_batch_dev(d, do, dl, n, ok, stream=s.cuda_stream)
+    s.synchronize()
+    okh = ok.cpu().numpy().astype(bool)
+    expect = np.ones(n, bool)
+    expect[bad] = False
+    np.testing.assert_array_equal(okh, expect)
+
+
+def test_full_size_cfg5_small_bit_exact(engine):
+    """BASELINE config 5 at full size (2^24 x 108-B frames, the lane-per-packet
+    kernel including its direct last batch): every word against the C oracle."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 24
+    buf, stride, flen = synth.uniform_frames(n, 64, seed=synth.SEED_CFG5)
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.compute_strided_dev(d, stride, flen, n, out, stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
