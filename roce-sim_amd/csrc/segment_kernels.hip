@@ -17,9 +17,10 @@
 // from the WR descriptor, payload dwords with one (unaligned) 16-byte MR load,
 // stores them with one aligned 16-byte store and folds them into its four CRC
 // columns and its UDP one's-complement sum in registers.  The frame is read
-// from the MR once and written once; nothing is read back.  Two chunks per
-// packet are held back until the group has combined its CRC and checksum: the
-// one holding the UDP checksum (dword 6) and the one holding the ICRC slot.
+// from the MR once and written once; nothing is read back.  The frame's first
+// and last iterations (one 128-byte line each at G = 8) are held back until
+// the group has combined its CRC and checksum, then stored whole with the UDP
+// checksum (dword 6) and the ICRC in place.
 //
 // Packet -> WR: a first small kernel writes each packet's WR index into the
 // `lens` output array (one workgroup per WR); the segmentation kernel reads
