@@ -409,8 +409,11 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   lds_u16* rlen = (lds_u16*)(uintptr_t)LD::kRlen;
   constexpr uint32_t kNoOff = 0xFFFFFFFFu;  // offset not representable: read it from HBM
 
-  for (uint32_t w0 = p0; w0 < p1; w0 += W) {
-    const int cnt = (int)min((uint32_t)W, p1 - w0);
+  // windows of equal size (<= W): no short last window with few sets per wave
+  const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
+  const uint32_t wsz = p1 > p0 ? (p1 - p0 + nwin - 1) / nwin : 1;
+  for (uint32_t w0 = p0; w0 < p1; w0 += wsz) {
+    const int cnt = (int)min(wsz, p1 - w0);
     if (tid < NB) hist[tid] = 0;
     __syncthreads();
     // iteration count of every packet of the window -> bucket
