@@ -18,7 +18,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-constexpr uint32_t kLdsMain = 131072;
 #ifndef RICRC_UNROLL
 #define RICRC_UNROLL 4
 #endif
@@ -81,7 +80,7 @@ __device__ __forceinline__ uint32_t pick4(const u32x4& w, int t, uint32_t dflt) 
 // (in-lane select + ds_bpermute), then R = sum_c' Mul(-32 c')(V_c'), as
 // three in-lane Horner steps with Mul(-32) and log2 G butterfly levels with
 // Mul(-128 * 2^l).
-template <int LOG2G>
+template <int LOG2G, class K>
 __device__ __forceinline__ uint32_t combine(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
                                            int r, int gl, int base) {
   constexpr int G = 1 << LOG2G;
@@ -101,12 +100,12 @@ __device__ __forceinline__ uint32_t combine(uint32_t a0, uint32_t a1, uint32_t a
     V2 = (uint32_t)__shfl((int)v2, m >= 2 ? s1 : s0, 64);
     V3 = (uint32_t)__shfl((int)v3, m >= 1 ? s1 : s0, 64);
   }
-  uint32_t B = mul_comb(V3, kLdsMain) ^ V2;
-  B = mul_comb(B, kLdsMain) ^ V1;
-  B = mul_comb(B, kLdsMain) ^ V0;
+  uint32_t B = mul_comb(V3, K::kComb) ^ V2;
+  B = mul_comb(B, K::kComb) ^ V1;
+  B = mul_comb(B, K::kComb) ^ V0;
 #pragma unroll
   for (int l = 0; l < LOG2G; ++l) {
-    const uint32_t mm = mul_comb(B, kLdsMain + 4096u * (1 + l));
+    const uint32_t mm = mul_comb(B, K::kComb + 4096u * (1 + l));
     const uint32_t t = ((gl >> l) & 1) ? mm : B;
     B = t ^ (uint32_t)__shfl_xor((int)t, 1 << l, 64);
   }
@@ -121,33 +120,111 @@ struct Col {
   uint32_t P[4], T[4];
 };
 
-__device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w, uint32_t kc0,
-                                       uint32_t kc1) {
+// Two LDS layouts of a byte-indexed table set (4 tables x 256 entries), both
+// conflict-free for ds_read_b32 and both one v_perm_b32 per address:
+//
+// Keys32: 32 copies, 128 KiB.  addr(tab, e, lane) = (tab >> 1) * 64 KiB +
+//   e * 256 + (tab & 1) * 128 + (lane & 31) * 4: every lane of a half-wave
+//   has its own copy (bank = lane & 31).
+// Keys16: 16 copies, 64 KiB.  addr(t, e, c) = e * 256 + t * 64 + c * 4,
+//   c = lane & 15.  Lanes l and l + 16 of a half-wave share copy c, so they
+//   read DIFFERENT tables in each of the four lookups (lane half
+//   h = (lane >> 4) & 1 reads table i ^ h, with byte i ^ h of the register,
+//   in lookup i): table t sits on banks (t & 1) * 16 + c and i ^ h flips that
+//   parity.  The XOR of the four lookups is the same in any order.  The
+//   per-lane byte choice lives in four v_perm selector registers.
+// The combine sets (Mul(-32), Mul(-128 * 2^l)) follow at kComb, unreplicated.
+struct Keys32 {
+  static constexpr uint32_t kComb = 131072;
+  uint32_t kc0, kc1;
+  __device__ static Keys32 make(int lane) {
+    const uint32_t k = (uint32_t)(lane & 31) << 2;
+    return Keys32{k, k | 0x10000u};
+  }
+  template <int THREADS>
+  __device__ static void stage(const uint32_t* m, int tid) {
+#pragma unroll
+    for (int r = 0; r < 8192 / THREADS; ++r) {
+      const int i = tid + r * THREADS;  // 8192 16-byte quads
+      const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
+      lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), m[tab * 256 + e]);
+    }
+  }
+  __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
+    const uint32_t x = xor3(P, T, w);
+    const uint32_t a0 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, kc1, 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, kc1, 0x0C020700u);
+    P = xor3(lds_rd(a0), lds_rd(a1 + 128), lds_rd(a2));
+    T = lds_rd(a3 + 128);
+  }
+};
+
+struct Keys16 {
+  static constexpr uint32_t kComb = 65536;
+  uint32_t ke, ko;          // byte 0: c * 4 + h * 64, c * 4 + (1 - h) * 64
+  uint32_t s0, s1, s2, s3;  // v_perm selectors: register byte (i ^ h) -> byte 1
+  __device__ static Keys16 make(int lane) {
+    const uint32_t c = (uint32_t)(lane & 15), h = (uint32_t)(lane >> 4) & 1u;
+    Keys16 k;
+    k.ke = c * 4u + h * 64u;
+    k.ko = c * 4u + (1u - h) * 64u;
+    k.s0 = 0x0C0C0000u | ((4u + (0u ^ h)) << 8);
+    k.s1 = 0x0C0C0000u | ((4u + (1u ^ h)) << 8);
+    k.s2 = 0x0C0C0000u | ((4u + (2u ^ h)) << 8);
+    k.s3 = 0x0C0C0000u | ((4u + (3u ^ h)) << 8);
+    return k;
+  }
+  template <int THREADS>
+  __device__ static void stage(const uint32_t* m, int tid) {
+    for (int i = tid; i < 4096; i += THREADS) {  // 1024 words x 4 quads of copies
+      const int w = i >> 2, q = i & 3;           // w = t * 256 + e
+      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + q * 16), m[w]);
+    }
+  }
+  __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
+    const uint32_t x = xor3(P, T, w);
+    const uint32_t a0 = __builtin_amdgcn_perm(x, ke, s0);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, ko, s1);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, ke, s2);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, ko, s3);
+    P = xor3(lds_rd(a0), lds_rd(a1), lds_rd(a2 + 128u));
+    T = lds_rd(a3 + 128u);
+  }
+};
+
+// The layout of the lane-group kernels (strided, ragged, segmentation).
+// Keys16 there (LDS-neutral for the 32x set's 64 KiB, larger ragged windows)
+// measured 2-4 % slower on mixed-MTU batches; the small kernel uses Keys16.
+#ifdef RICRC_TABLES16
+using MainKeys = Keys16;
+#else
+using MainKeys = Keys32;
+#endif
+
+template <class K>
+__device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w, const K& k) {
 #ifdef RICRC_ABLATE_FOLD  // diagnostic build only: loads kept, table folding removed
   P ^= w;
 #else
-  const uint32_t x = xor3(P, T, w);
-  const uint32_t a0 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(x, kc1, 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(x, kc1, 0x0C020700u);
-  P = xor3(lds_rd(a0), lds_rd(a1 + 128), lds_rd(a2));
-  T = lds_rd(a3 + 128);
+  k.absorb(P, T, w);
 #endif
 }
 
-__device__ __forceinline__ void fold(Col& c, const u32x4& w, uint32_t kc0, uint32_t kc1) {
-  absorb(c.P[0], c.T[0], w.x, kc0, kc1);
-  absorb(c.P[1], c.T[1], w.y, kc0, kc1);
-  absorb(c.P[2], c.T[2], w.z, kc0, kc1);
-  absorb(c.P[3], c.T[3], w.w, kc0, kc1);
+template <class K>
+__device__ __forceinline__ void fold(Col& c, const u32x4& w, const K& k) {
+  absorb(c.P[0], c.T[0], w.x, k);
+  absorb(c.P[1], c.T[1], w.y, k);
+  absorb(c.P[2], c.T[2], w.z, k);
+  absorb(c.P[3], c.T[3], w.w, k);
 }
 
 // The packet's last iteration: columns past the end (k >= n) keep their register.
-__device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n, uint32_t kc0,
-                                          uint32_t kc1) {
+template <class K>
+__device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n, const K& k) {
   Col f = c;
-  fold(f, w, kc0, kc1);
+  fold(f, w, k);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     c.P[t] = (kb + t < n) ? f.P[t] : c.P[t];
@@ -155,23 +232,20 @@ __device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n,
   }
 }
 
-// LDS staging of the folding tables (every kernel, once per workgroup).
-template <int LOG2G, int THREADS = 1024>
+// LDS address of the IHL-5 fix-up table (after the combine sets).
+template <int LOG2G, class K>
+constexpr uint32_t kFixLut = K::kComb + 4096u * (1 + LOG2G);
+
+// LDS staging of the folding tables (every lane-group kernel, once per workgroup).
+template <int LOG2G, int THREADS, class K>
 __device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
   constexpr int NCOMB = 1 + LOG2G;
-  const uint32_t* gm = tables + LOG2G * 1024;
-#pragma unroll
-  for (int r = 0; r < 8192 / THREADS; ++r) {
-    const int i = tid + r * THREADS;  // 8192 16-byte quads
-    const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
-    lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16),
-            gm[tab * 256 + e]);
-  }
+  K::template stage<THREADS>(tables + LOG2G * 1024, tid);
   const uint32_t* gc = tables + kNumMainSets * 1024;
-  for (int i = tid; i < NCOMB * 1024; i += THREADS) lds_wr(kLdsMain + 4u * i, gc[i]);
+  for (int i = tid; i < NCOMB * 1024; i += THREADS) lds_wr(K::kComb + 4u * i, gc[i]);
   if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
     const int k = tid - 3;
-    const uint32_t lut = kLdsMain + 4096u * NCOMB;
+    const uint32_t lut = kFixLut<LOG2G, K>;
     const uint32_t andm = k < 0 ? 0u : ~0u;
     const uint32_t orm = k == 0 ? 0x0000FF00u : k == 2 ? 0xFFFF00FFu : k == 6 ? 0xFFFF0000u
                          : k == 8 ? 0x000000FFu : 0u;

@@ -32,6 +32,8 @@
 //                 (bank = lane & 31, conflict-free); the address is ONE
 //                 v_perm_b32 of the register and a per-lane constant.
 //   [128 KiB, +4 KiB * (1 + log2 G))  combine tables, unreplicated.
+//   (icrc_device.hpp: Keys32; the 16-copy Keys16 layout is an option there
+//   and the layout of the small-frame kernel.)
 //
 // Masks, seed: the masked dwords are packet dwords 0 (TOS), 2 (TTL, IP csum),
 // IHL+1 (UDP csum) and IHL+3 (BTH byte 4); the FF x 8 prefix is folded in as
@@ -148,8 +150,7 @@ __device__ __forceinline__ void fix_chunk(u32x4& w, int kb, int kub, int kbb, ui
 // Recomputation of one packet by its group with the masks of a general IHL
 // (IPv4 options).  Rare path: the main loop applies the IHL-5 masks.
 template <int LOG2G>
-__device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, uint32_t kc0,
-                                             uint32_t kc1) {
+__device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, MainKeys kk) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   const int kub = ihl + 1, kbb = ihl + 3;
@@ -160,12 +161,12 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, u
     u32x4 w = load_chunk<G>(p, j, gl);
     fix_chunk(w, kb, kub, kbb, h0, h2);
     if (j == p.J - 1)
-      fold_last(A, w, kb, p.n, kc0, kc1);
+      fold_last(A, w, kb, p.n, kk);
     else
-      fold(A, w, kc0, kc1);
+      fold(A, w, kk);
   }
-  return combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2], A.P[3] ^ A.T[3], p.r,
-                        gl, base);
+  return combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                  A.P[3] ^ A.T[3], p.r, gl, base);
 }
 
 
@@ -206,22 +207,22 @@ struct OutBuf {
   uint32_t p0, cap;
 };
 template <int LOG2G>
-constexpr uint32_t kOutLds = kLdsMain + 4096u * (1 + LOG2G) + 256u;  // after the fix-up LUT
+constexpr uint32_t kOutLds = kFixLut<LOG2G, MainKeys> + 256u;  // after the fix-up LUT
 
 template <int LOG2G, bool VERIFY>
 __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
-                                            int base, uint32_t kc0, uint32_t kc1, OutBuf ob);
+                                            int base, const MainKeys& kk, OutBuf ob);
 
 // Fold, combine, check and emit one packet whose first batch is in `b`.
 template <int LOG2G, bool VERIFY>
 __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, Batch<kUnroll>& b,
-                                              int gl, int base, uint32_t kc0, uint32_t kc1,
+                                              int gl, int base, const MainKeys& kk,
                                               OutBuf ob = {0, 0}) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   constexpr int U = kUnroll;
-  constexpr uint32_t kLut = kLdsMain + 4096u * (1 + LOG2G);
+  constexpr uint32_t kLut = kFixLut<LOG2G, MainKeys>;
   // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
   // U (the first block holds the remainder), then the last one (J-1), which
   // skips columns past the end and may also need the fix-ups.
@@ -236,7 +237,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   for (int j = 0; j < jhh; ++j) {
     u32x4 w = (j == 0) ? b.wh0 : (j == 1) ? b.wh1 : load_chunk<G>(p, j, gl);
     fix_chunk5(w, DPI * j + 4 * gl - p.S, kLut, h0, h2);
-    fold(A, w, kc0, kc1);
+    fold(A, w, kk);
   }
   // body blocks, ping-pong between b.cur and nxt (no register copies)
   int j0 = jhh, bs = first;
@@ -249,7 +250,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (u < bs) fold(A, b.cur[u], kc0, kc1);
+      if (u < bs) fold(A, b.cur[u], kk);
     if (bk + 1 >= nblk) break;
     j0 = jn;
     jn = j0 + U;
@@ -258,7 +259,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
       for (int u = 0; u < U; ++u) b.cur[u] = load_body<G>(p, jn + u, gl);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) fold(A, nxt[u], kc0, kc1);
+    for (int u = 0; u < U; ++u) fold(A, nxt[u], kk);
     j0 = jn;
     bs = U;
   }
@@ -266,20 +267,20 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     u32x4 w = b.wl;
     const int kb = DPI * JL + 4 * gl - p.S;
     if (JL < p.jh) fix_chunk5(w, kb, kLut, h0, h2);
-    fold_last(A, w, kb, p.n, kc0, kc1);
+    fold_last(A, w, kb, p.n, kk);
   }
-  emit_packet<LOG2G, VERIFY>(a, p, A, h0, h2, b.trailer, gl, base, kc0, kc1, ob);
+  emit_packet<LOG2G, VERIFY>(a, p, A, h0, h2, b.trailer, gl, base, kk, ob);
 }
 
 // Packet done: fold the group's columns, check the header, emit.
 template <int LOG2G, bool VERIFY>
 __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
-                                            int base, uint32_t kc0, uint32_t kc1, OutBuf ob) {
+                                            int base, const MainKeys& kk, OutBuf ob) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
-  uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
-                              A.P[3] ^ A.T[3], p.r, gl, base);
+  uint32_t B = combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                        A.P[3] ^ A.T[3], p.r, gl, base);
   const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
   const uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
   uint32_t st = p.dead ? kPktBadLen : 0u;
@@ -295,7 +296,7 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
     if (tot != p.L) st |= kPktLenMismatch;
   }
   const bool good = (st & kPktFatal) == 0;
-  if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kc0, kc1);
+  if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kk);
   const uint32_t icrc = good ? ~B : 0u;
   if (p.live && gl == 0) {
     if constexpr (VERIFY) {
@@ -320,14 +321,13 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;  // packets per wave step
   const int tid = threadIdx.x;
-  stage_tables<LOG2G, kIcrcThreads>(a.tables, tid);
+  stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
   const int grp = lane >> LOG2G;
-  const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
-  const uint32_t kc1 = kc0 | 0x10000u;
+  const MainKeys kk = MainKeys::make(lane);
   // Each workgroup owns a contiguous range of packet sets, so every CU sweeps
   // one contiguous region of HBM (measured: 6.8 vs 5.6 TB/s for
   // grid-interleaved sets); its 16 waves take consecutive sets of that range.
@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kIcrcWaves) {
     const Pkt p = make(set);
     Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
-    finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kc0, kc1, ob);
+    finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk, ob);
   }
   if (a.icrc_out) {  // (uniform)
     __syncthreads();
@@ -366,18 +366,18 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
 // Ragged frames (offsets[i], lens[i]).  The lanes of a wave fold their
 // packets in lockstep, so a wave waits for the longest packet of its set.
 // Each workgroup therefore takes a contiguous window of packets (locality
-// kept) and counting-sorts it in LDS by iteration count; waves then take
-// size-homogeneous sets of the sorted window, round robin.
+// kept) and counting-sorts it in LDS by iteration count; waves then claim
+// size-homogeneous sets of the sorted window from both ends.
 template <int LOG2G>
 struct RaggedLds {
   static constexpr int kNComb = 1 + LOG2G;
-  static constexpr uint32_t kBase = kLdsMain + 4096u * kNComb + 256u;  // after the fix-up LUT
+  static constexpr uint32_t kBase = kFixLut<LOG2G, MainKeys> + 256u;  // after the fix-up LUT
   static constexpr int kBuckets = 128;
   static constexpr uint32_t kHist = kBase;               // kBuckets x u32 counts / cursors
   static constexpr uint32_t kPerm = kBase + 4 * kBuckets;  // window x u16 local indices
   static constexpr int kAvail = (int)(163840u - kPerm);
   // sorted descriptors: u16 local index, u32 offset / 4, u16 length (8 B)
-  static constexpr int kWindow = (kAvail / 8 >= 4096) ? 4096 : (kAvail / 8) / 64 * 64;
+  static constexpr int kWindow = (kAvail / 8 >= 8192) ? 8192 : (kAvail / 8) / 64 * 64;
   static constexpr uint32_t kRoff = kPerm + 2 * kWindow;
   static constexpr uint32_t kRlen = kRoff + 4 * kWindow;
   static constexpr uint32_t kBytes = kRlen + 2 * kWindow;
@@ -391,14 +391,14 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   using LD = RaggedLds<LOG2G>;
   constexpr int W = LD::kWindow;
   constexpr int NB = LD::kBuckets;
+  static_assert(W + kIcrcWaves < 65536, "set claims are 16-bit counters");
   const int tid = threadIdx.x;
-  stage_tables<LOG2G, kIcrcThreads>(a.tables, tid);
+  stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
 
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
   const int grp = lane >> LOG2G;
-  const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
-  const uint32_t kc1 = kc0 | 0x10000u;
+  const MainKeys kk = MainKeys::make(lane);
   const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
   const uint32_t p0 = blockIdx.x * per_block;
   const uint32_t p1 = min(a.n, p0 + per_block);
@@ -408,6 +408,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   lds_u32* roff = (lds_u32*)(uintptr_t)LD::kRoff;
   lds_u16* rlen = (lds_u16*)(uintptr_t)LD::kRlen;
   constexpr uint32_t kNoOff = 0xFFFFFFFFu;  // offset not representable: read it from HBM
+  lds_u32* claim = (lds_u32*)(uintptr_t)(LD::kBase - 4u);  // (free word at the end of the LUT)
+  const bool from_back = ((tid >> 6) & 1) != 0;
 
   // windows of equal size (<= W): no short last window with few sets per wave
   const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
@@ -415,6 +417,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   for (uint32_t w0 = p0; w0 < p1; w0 += wsz) {
     const int cnt = (int)min(wsz, p1 - w0);
     if (tid < NB) hist[tid] = 0;
+    if (tid == NB) *claim = 0;
     __syncthreads();
     // iteration count of every packet of the window -> bucket
     constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
@@ -473,10 +476,24 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
       const uint64_t off = ow != kNoOff ? (uint64_t)ow << 2 : a.offsets[pkt];
       return describe<DPI>(a.frames, pkt, live, live ? off : 0, live ? (uint32_t)rlen[ix] : 0);
     };
-    for (int set = tid >> 6; set < nsets; set += kIcrcWaves) {
+    // Dynamic claims from both ends of the sorted window (one LDS atomic per
+    // set on a packed front | back << 16 counter): even waves take the short
+    // sets, odd waves the long ones, so a CU mixes instruction-bound and
+    // load-bound sets, and no wave idles at the window barrier while sets
+    // remain.  Measured against round robin: cfg3 +3-6 %, 2 KiB frames +3 %,
+    // 256 B +5 %; a quarter or three quarters of the waves taking the long
+    // sets, or claiming the next set before finishing the current one, were
+    // no better.
+    for (;;) {
+      uint32_t old = 0;
+      if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? 0x10000u : 1u);
+      old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+      const int f = (int)(old & 0xFFFFu), bk = (int)(old >> 16);
+      if (f + bk >= nsets) break;
+      const int set = from_back ? nsets - 1 - bk : f;
       const Pkt p = make(set);
       Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
-      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kc0, kc1);
+      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk);
     }
     __syncthreads();
   }
@@ -505,49 +522,13 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 // the prefetch.  Hence unconditional LDS writes into the slot and the masks
 // applied in LDS rather than by uniform selects in the loop.
 //
-// LDS: [0, 64 KiB) Mul(128) replicated 16x, [64, 68 KiB) Mul(-32), then one
-// staging slot of 64 x stride bytes per wave.  Replica layout: entry e of
-// table t, copy c at e * 256 + t * 64 + c * 4 (c = lane & 15).  Lanes l and
-// l + 16 of a ds_read_b32 half-wave share copy c, so they read DIFFERENT
-// tables in each of the four lookups (lane half h = (lane >> 4) & 1 reads
-// table i ^ h in lookup i): table t sits on banks (t & 1) * 16 + c, and
-// i ^ h flips that parity, so the half-wave is conflict-free.  The XOR of
-// the four lookups is the same in any order.  Each address is ONE v_perm_b32
-// (x byte (i ^ h) -> byte 1, the per-lane copy/table offset -> byte 0) with
-// per-lane selector registers; the odd lookups' table offset is folded into
-// their own constant, the upper pair's 128 into the instruction offset.
+// LDS: [0, 64 KiB) Mul(128) in the Keys16 layout (icrc_device.hpp: 16
+// conflict-free copies, one v_perm_b32 per address), [64, 68 KiB) Mul(-32),
+// then one staging slot of 64 x stride bytes per wave.
 constexpr int kSmallMaxWaves = 12;
-constexpr uint32_t kSmallComb = 65536;
+constexpr uint32_t kSmallComb = Keys16::kComb;
 constexpr uint32_t kSmallStage = kSmallComb + 4096;
 constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + 3) / 4;  // ns <= 8
-
-struct SmallKeys {
-  uint32_t ke, ko;              // byte 0: c * 4 + h * 64, c * 4 + (1 - h) * 64
-  uint32_t s0, s1, s2, s3;      // v_perm selectors: x byte (i ^ h) -> byte 1
-};
-
-__device__ __forceinline__ SmallKeys small_keys(int lane) {
-  const uint32_t c = (uint32_t)(lane & 15), h = (uint32_t)(lane >> 4) & 1u;
-  SmallKeys k;
-  k.ke = c * 4u + h * 64u;
-  k.ko = c * 4u + (1u - h) * 64u;
-  k.s0 = 0x0C0C0000u | ((4u + (0u ^ h)) << 8);
-  k.s1 = 0x0C0C0000u | ((4u + (1u ^ h)) << 8);
-  k.s2 = 0x0C0C0000u | ((4u + (2u ^ h)) << 8);
-  k.s3 = 0x0C0C0000u | ((4u + (3u ^ h)) << 8);
-  return k;
-}
-
-// (P, T) <- Mul(128)(P ^ T ^ w) from the 16x set (P = three lookups, T = the fourth)
-__device__ __forceinline__ void absorb16(uint32_t& P, uint32_t& T, uint32_t w, const SmallKeys& k) {
-  const uint32_t x = xor3(P, T, w);
-  const uint32_t a0 = __builtin_amdgcn_perm(x, k.ke, k.s0);
-  const uint32_t a1 = __builtin_amdgcn_perm(x, k.ko, k.s1);
-  const uint32_t a2 = __builtin_amdgcn_perm(x, k.ke, k.s2);
-  const uint32_t a3 = __builtin_amdgcn_perm(x, k.ko, k.s3);
-  P = xor3(lds_rd(a0), lds_rd(a1), lds_rd(a2 + 128u));
-  T = lds_rd(a3 + 128u);
-}
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
@@ -567,7 +548,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  const SmallKeys kk = small_keys(lane);
+  const Keys16 kk = Keys16::make(lane);
   const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch (<= 64 C)
   const uint32_t nw = blockDim.x >> 6;
   const uint32_t stage = kSmallStage + (uint32_t)wave * 64u * S;
@@ -621,7 +602,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
         for (int c = 0; c < 4; ++c) {
           const int k = 4 * j + c - pad;
           const uint32_t w = rd(k < 0 ? 0 : k, 4 * j + c);  // (never read before the frame)
-          absorb16(P[c], T[c], (j == 0 && k < 0) ? 0u : w, kk);
+          kk.absorb(P[c], T[c], (j == 0 && k < 0) ? 0u : w);
         }
       }
     }

@@ -280,15 +280,14 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
   constexpr int PPW = 64 / G;
   constexpr int U = kSegUnroll;
   const int tid = threadIdx.x;
-  stage_tables<LOG2G, kSegThreads>(a.tables, tid);
+  stage_tables<LOG2G, kSegThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
   const int grp = lane >> LOG2G;
   const int base = grp * G;
-  const uint32_t kc0 = (uint32_t)(lane & 31) << 2;
-  const uint32_t kc1 = kc0 | 0x10000u;
+  const MainKeys kk = MainKeys::make(lane);
   const uint8_t* mr_end = a.mr + a.mr_bytes;
   // lowest start of a 16-byte read that stays inside the MR (an MR shorter
   // than 16 bytes must be readable for 16, include/roce_icrc.h)
@@ -356,9 +355,9 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
         w.z = fix_dword(w.z, idx0 + 2, 6, 8);
         w.w = fix_dword(w.w, idx0 + 3, 6, 8);
         if (j == J - 1)
-          fold_last(A, w, idx0, n, kc0, kc1);
+          fold_last(A, w, idx0, n, kk);
         else
-          fold(A, w, kc0, kc1);
+          fold(A, w, kk);
       }
     };
     // block b >= 1: the full-payload fast path when all its iterations lie in
@@ -371,7 +370,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
         for (int u = 0; u < U; ++u) {
           __builtin_nontemporal_store(v[u], (u32x4*)(d + 4 * DPI * u));
           csum_add(acc, v[u]);
-          fold(A, v[u], kc0, kc1);
+          fold(A, v[u], kk);
         }
       } else {
 #pragma unroll
@@ -433,8 +432,8 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
       run(std::false_type{});
 
     // ---- group combine: ICRC, then the UDP checksum over the final bytes -----
-    const uint32_t B = combine<LOG2G>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
-                                      A.P[3] ^ A.T[3], r, gl, base);
+    const uint32_t B = combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                                A.P[3] ^ A.T[3], r, gl, base);
     const uint32_t icrc = ~B;
     uint32_t f = (uint32_t)acc;
     f = (f & 0xFFFFu) + (f >> 16) + (uint32_t)(acc >> 32);
@@ -514,7 +513,7 @@ seg_fn select_segment(int log2g) {
   }
 }
 
-size_t seg_lds_bytes(int log2g) { return kLdsMain + 4096u * (1 + log2g) + 256u; }
+size_t seg_lds_bytes(int log2g) { return MainKeys::kComb + 4096u * (1 + log2g) + 256u; }
 
 }  // namespace
 
