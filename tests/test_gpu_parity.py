@@ -375,3 +375,68 @@ def test_full_size_cfg5_small_bit_exact(engine):
     engine.compute_strided_dev(d, stride, flen, n, out, stream=s.cuda_stream)
     s.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def test_ragged_many_windows_random_sizes(engine):
+    """The ragged kernel over 2^21 frames of random length (44 .. 1020 B, so
+    every workgroup sorts several windows and claims sets from both ends of
+    each), laid out in memory order with malformed frames scattered in:
+    lengths not a multiple of 4, TCP instead of UDP, an IP total length that
+    disagrees with the frame, IPv4 options.  Lane settings 4, 8 and 16;
+    compute and verify against the C oracle."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(2024)
+    n = 1 << 21
+    lens = (rng.integers(11, 256, n) * 4).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1], out=offs[1:])
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1]), dtype=np.uint8)
+    o64 = offs.astype(np.int64)
+    buf[o64] = 0x45
+    tot = lens.copy()
+    mism = rng.choice(n, 500, replace=False)
+    tot[mism] += 4
+    buf[o64 + 2] = (tot >> 8).astype(np.uint8)
+    buf[o64 + 3] = (tot & 0xFF).astype(np.uint8)
+    buf[o64 + 9] = 17
+    tcp = rng.choice(n, 500, replace=False)
+    buf[o64[tcp] + 9] = 6
+    opt = rng.choice(n, 500, replace=False)
+    buf[o64[opt]] = 0x46
+    odd = rng.choice(n, 500, replace=False)
+    lens_k = lens.copy()
+    lens_k[odd] -= 2  # ends 2 bytes early: not a multiple of 4
+    want, _ = oracle_batch(buf, offsets=offs, lens=lens)
+    good = np.ones(n, bool)
+    good[odd] = False
+    # trailers = the oracle's words (frames it rejects keep 0 there, and so
+    # fail verification like on the GPU); then one payload bit of every 1013th
+    trail = o64 + lens.astype(np.int64) - 4
+    buf[(trail[:, None] + np.arange(4)[None, :]).reshape(-1)] = want.view(np.uint8)
+    flip = np.arange(5, n, 1013)
+    buf[o64[flip] + 40] ^= 0x08
+    want, ok_want = oracle_batch(buf, offsets=offs, lens=lens)
+    fatal = np.zeros(n, bool)
+    fatal[tcp] = True
+    fatal[odd] = True
+    d = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens_k.view(np.int32)).cuda()
+    s = torch.cuda.current_stream()
+    for lanes in (4, 8, 16):
+        engine.set_lanes(lanes)
+        try:
+            out = torch.zeros(n, dtype=torch.int32, device="cuda")
+            ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            engine.compute_batch_dev(d, do, dl, n, out, stream=s.cuda_stream)
+            engine.verify_batch_dev(d, do, dl, n, ok, stream=s.cuda_stream)
+            s.synchronize()
+        finally:
+            engine.set_lanes(0)
+        got = out.cpu().numpy().view(np.uint32)
+        okh = ok.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(got[good], want[good], err_msg=f"lanes {lanes}")
+        assert (got[odd] == 0).all()
+        exp_ok = ok_want.astype(bool) & ~fatal
+        np.testing.assert_array_equal(okh, exp_ok, err_msg=f"lanes {lanes}")
+        assert not okh[flip].any() and okh.sum() > n - 4000
