@@ -5,24 +5,25 @@
 // FF x 8 || frame[0 : len-4] with IP tos/ttl/chksum, UDP chksum and the BTH
 // fecn|becn|resv6 byte forced to ones (src/roce.py:204-211).
 //
-// Work decomposition ("end-aligned dword grid").  A group of G lanes
-// (G = 1 .. 64, a power of two) owns one packet.  The packet's n covered
-// dwords are laid on a grid of J iterations x 4G dwords whose LAST dword is
-// the packet's last covered dword (pad = 4GJ - n zero dwords at the front,
-// which do not change a zero-initialised CRC register).  In iteration j, lane
-// i of the group reads the 16 contiguous bytes at grid dwords 4Gj + 4i .. +3
-// with one dwordx4 load, so a group reads 16G contiguous bytes per
-// instruction and a wave reads 64/G such runs.  Each lane keeps four CRC
-// registers a_t (t = grid column inside the lane) and folds
+// Work decomposition ("absolute-aligned dword grid").  A group of G lanes
+// (G = 1 .. 64, a power of two) owns one packet.  Its n covered dwords are
+// laid on a grid of J iterations x 4G dwords aligned to ABSOLUTE memory:
+// iteration j covers the dwords [ab/4 + 4G j, ab/4 + 4G (j + 1)), ab = the
+// frame start rounded down to 16G bytes, so in iteration j lane i of the
+// group reads ONE aligned 16-byte chunk and the group an aligned 16G-byte
+// run.  Columns before the frame start hold zero (a zero register stays
+// zero); columns past its end skip the last iteration.  Each lane keeps four
+// CRC registers a_t (t = grid column inside the lane) and folds
 //
 //      a_t <- Mul(128 G)(a_t ^ w_t)          (= "w_t followed by 16G-4 zero bytes")
 //
 // where Mul(m) is multiplication by x^m mod P on the reflected register,
-// evaluated as four byte-indexed table lookups from LDS.  At the end the
-// register of grid column s = 4i + t is off by exactly x^(32 s), so the
-// packet CRC is  R = sum_s Mul(-32 s)(a_s): three in-lane Horner steps with
-// Mul(-32) and log2 G cross-lane butterfly levels with Mul(-128 * 2^l)
-// (__shfl_xor inside the group).  No MFMA: this is a byte scan, bound by HBM.
+// evaluated as four byte-indexed table lookups from LDS.  The packet ends at
+// column r of its last iteration, so column c is off by x^(32 ((c - r) mod
+// 4G)): combine() rotates the columns by r and folds R = sum Mul(-32 c')(a_c')
+// with three in-lane Horner steps (Mul(-32)) and log2 G cross-lane butterfly
+// levels (Mul(-128 * 2^l), __shfl_xor inside the group).  No MFMA: this is a
+// byte scan, bound by HBM.
 //
 // LDS (per workgroup, one 1024-thread workgroup per CU):
 //   [0, 128 KiB)  Mul(128 G) tables replicated 32x so every lane of a
