@@ -312,7 +312,9 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
       else
         a.icrc_out[p.pkt] = icrc;
     }
+#ifndef RICRC_BLOCK_TIMES
     if (a.status_out) a.status_out[p.pkt] = (uint8_t)st;
+#endif
   }
 }
 
@@ -322,6 +324,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;  // packets per wave step
   const int tid = threadIdx.x;
+#ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 
@@ -362,6 +367,13 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
     for (uint32_t i = (uint32_t)tid; i < ob.cap; i += kIcrcThreads)
       a.icrc_out[p0 + i] = lds_rd(kOutLds<LOG2G> + 4u * i);
   }
+#ifdef RICRC_BLOCK_TIMES
+  __syncthreads();
+  if (tid == 0 && a.status_out) {
+    ((uint64_t*)a.status_out)[2 * blockIdx.x] = t_start;
+    ((uint64_t*)a.status_out)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // Ragged frames (offsets[i], lens[i]).  The lanes of a wave fold their
@@ -394,6 +406,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   constexpr int NB = LD::kBuckets;
   static_assert(W + kIcrcWaves < 65536, "set claims are 16-bit counters");
   const int tid = threadIdx.x;
+#ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
 
   const int lane = tid & 63;
@@ -498,6 +513,12 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
     }
     __syncthreads();
   }
+#ifdef RICRC_BLOCK_TIMES
+  if (tid == 0 && a.status_out) {
+    ((uint64_t*)a.status_out)[2 * blockIdx.x] = t_start;
+    ((uint64_t*)a.status_out)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
