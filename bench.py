@@ -85,6 +85,18 @@ def _cpu_chunk(se):
                     np.uint32)
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (record it with the core count)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: np.ndarray):
     """Per-packet zlib restatement (oracle/, the CPU "port" baseline) on this host.
 
@@ -132,6 +144,7 @@ def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: 
                    f"pool ({tn:.2f} s); "
                    f"single core {n1} packets {c_one / t1 / 2**30:.3f} GiB/s"),
         "single_core_GiBps": round(c_one / t1 / 2**30, 4),
+        "cpu_model": cpu_model(),
         "parity_mismatches_vs_gpu": mism,
     }
 
@@ -298,6 +311,7 @@ def cpu_baseline_seg(mr: np.ndarray, rec: np.ndarray, pmtu: int, frames_ok):
         "sample": (f"Python restatement of process_send_req + IPv4/UDP/BTH serialisation + "
                    f"zlib ICRC per packet (oracle/segment_oracle.py): {nw} WRs = "
                    f"{nw * (SEG_MSG // pmtu)} packets on a {procs}-process fork pool ({tn:.2f} s)"),
+        "cpu_model": cpu_model(),
         "parity_mismatches_vs_gpu": mism,
     }
 
