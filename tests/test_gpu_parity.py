@@ -440,3 +440,87 @@ def test_ragged_many_windows_random_sizes(engine):
         exp_ok = ok_want.astype(bool) & ~fatal
         np.testing.assert_array_equal(okh, exp_ok, err_msg=f"lanes {lanes}")
         assert not okh[flip].any() and okh.sum() > n - 4000
+
+
+def test_offsets_above_16_gib(engine):
+    """Frames placed beyond 2^34 bytes into one 17-GiB device buffer.  The
+    ragged kernel keeps sorted offsets as u32 dwords (< 16 GiB) and takes a
+    larger offset from the descriptor array in HBM instead; this interleaves
+    both kinds in every sort window, for compute and verify, at lanes 4/8/16,
+    against the C oracle (the HBM layout is sized for 288 GB per GPU)."""
+    torch = pytest.importorskip("torch")
+    n = 20000
+    lo_buf, lo_offs, lens_a = synth.mixed_mtu_frames(n, seed=41)
+    hi_buf, hi_offs, lens_b = synth.mixed_mtu_frames(n, seed=42)
+    want_a, _ = oracle_batch(lo_buf, offsets=lo_offs, lens=lens_a)
+    want_b, _ = oracle_batch(hi_buf, offsets=hi_offs, lens=lens_b)
+    hi0 = (1 << 34) + 4096 + 12  # dword- but not 16-byte-aligned base
+    d = torch.empty(hi0 + hi_buf.size, dtype=torch.uint8, device="cuda")
+    d[:lo_buf.size].copy_(torch.from_numpy(lo_buf))
+    d[hi0:hi0 + hi_buf.size].copy_(torch.from_numpy(hi_buf))
+    offs = np.empty(2 * n, np.uint64)
+    offs[0::2] = lo_offs
+    offs[1::2] = hi_offs + np.uint64(hi0)
+    lens = np.empty(2 * n, np.uint32)
+    lens[0::2], lens[1::2] = lens_a, lens_b
+    want = np.empty(2 * n, np.uint32)
+    want[0::2], want[1::2] = want_a, want_b
+    # trailers = the words, then one payload bit of every 101st frame flipped
+    for buf, off, ln, w, base in ((lo_buf, lo_offs, lens_a, want_a, 0),
+                                  (hi_buf, hi_offs, lens_b, want_b, hi0)):
+        t = off.astype(np.int64) + ln.astype(np.int64) - 4
+        buf[(t[:, None] + np.arange(4)[None, :]).reshape(-1)] = w.view(np.uint8)
+        buf[off[::101].astype(np.int64) + 48] ^= 0x10
+        d[base:base + buf.size].copy_(torch.from_numpy(buf))
+    expect_ok = np.ones(2 * n, bool)
+    expect_ok[0::2][::101] = False
+    expect_ok[1::2][::101] = False
+    flips = torch.from_numpy(np.concatenate(
+        [lo_offs[::101].astype(np.int64) + 48, hi_offs[::101].astype(np.int64) + 48 + hi0])).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    s = torch.cuda.current_stream()
+    try:
+        for lanes in (4, 8, 16):
+            engine.set_lanes(lanes)
+            out = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+            ok = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+            icrc_v = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+            engine.verify_batch_dev(d, do, dl, 2 * n, ok, icrc_v, stream=s.cuda_stream)
+            s.synchronize()
+            np.testing.assert_array_equal(ok.cpu().numpy().astype(bool), expect_ok,
+                                          err_msg=f"lanes {lanes}")
+            d[flips] ^= 0x10  # restore the flipped bits: every computed word bit-exact
+            engine.compute_batch_dev(d, do, dl, 2 * n, out, stream=s.cuda_stream)
+            s.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want,
+                                          err_msg=f"lanes {lanes}")
+            d[flips] ^= 0x10
+    finally:
+        engine.set_lanes(0)
+        del d
+        torch.cuda.empty_cache()
+
+
+def test_small_kernel_beyond_4_gib(engine):
+    """The lane-per-packet kernel over 42 x 999983 frames of 128 B (5.4 GB,
+    stride = the small kernel's maximum): batch and frame addresses cross
+    2^32 bytes.  The buffer tiles a prime number of distinct frames, so an
+    address that wrapped at 2^32 would read a frame with a different ICRC;
+    every word is checked against the tiled C-oracle result."""
+    torch = pytest.importorskip("torch")
+    m, reps = 999983, 42
+    buf, stride, flen = synth.uniform_frames(m, 84, seed=synth.SEED_CFG5)
+    assert stride == 128
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=m)
+    n = m * reps
+    d = torch.from_numpy(buf).cuda().repeat(reps)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.compute_strided_dev(d, stride, flen, n, out, stream=s.cuda_stream)
+    s.synchronize()
+    got = out.cpu().numpy().view(np.uint32).reshape(reps, m)
+    bad = np.nonzero((got != want[None, :]).any(axis=1))[0]
+    assert bad.size == 0, f"tiles with wrong words: {bad.tolist()}"
+    del d
+    torch.cuda.empty_cache()
