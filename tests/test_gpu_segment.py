@@ -232,3 +232,49 @@ def test_full_size_batch_properties(engine):
         assert O.inet_checksum(f[:20]) == 0
         pseudo = f[12:20] + struct.pack("!BBH", 0, 17, len(f) - 20)
         assert O.inet_checksum(pseudo + f[20:]) == 0
+
+
+def test_mr_offsets_beyond_4_gib(engine):
+    """A 4 GiB + 1 MiB device MR: WRs that straddle 2^32, start above it and
+    end exactly at the MR end are segmented bit-exactly (64-bit MR offsets;
+    the MR-end guard above 2^32).  The oracle sees the same bytes rebased to
+    a small host array (frames carry no MR offset)."""
+    import torch
+
+    pmtu = 1024
+    mr_bytes = (1 << 32) + (1 << 20)
+    base = (1 << 32) - 8192
+    tail = np.random.default_rng(99).integers(0, 256, mr_bytes - base, dtype=np.uint8)
+    spans = [((1 << 32) - 3001, 9000, SO.SEND), ((1 << 32) + 77, 3 * pmtu + 5, SO.RDMA_WRITE),
+             (mr_bytes - (2 * pmtu + 13), 2 * pmtu + 13, SO.READ_RESPONSE)]
+    wrs = [SO.SegWR(op=op, mr_offset=off, length=ln, psn=100 * i, dqpn=0x21, src_ip=SRC_IP,
+                    dst_ip=DST_IP, sport=5, flags=SO.SIGNALED)
+           for i, (off, ln, op) in enumerate(spans)]
+    rebased = [SO.SegWR(op=w.op, mr_offset=w.mr_offset - base, length=w.length, psn=w.psn,
+                        dqpn=w.dqpn, src_ip=w.src_ip, dst_ip=w.dst_ip, sport=w.sport,
+                        flags=w.flags) for w in wrs]
+    want = SO.segment(tail.tobytes(), rebased, pmtu)
+    rec = to_records(wrs)
+    npkts, slot = E.segment_plan(rec, pmtu)
+    assert npkts == len(want)
+    dev = torch.device("cuda", 0)
+    d_mr = torch.empty(mr_bytes, dtype=torch.uint8, device=dev)
+    d_mr[base:].copy_(torch.from_numpy(tail))
+    d_wrs = torch.from_numpy(rec.view(np.uint8)).to(dev)
+    d_frames = torch.zeros(npkts * slot, dtype=torch.uint8, device=dev)
+    d_lens = torch.zeros(npkts, dtype=torch.int32, device=dev)
+    d_icrc = torch.zeros(npkts, dtype=torch.int32, device=dev)
+    d_st = torch.zeros(npkts, dtype=torch.uint8, device=dev)
+    engine.segment_dev(d_mr, mr_bytes, d_wrs, len(wrs), pmtu, npkts, d_frames, slot, d_lens,
+                       d_icrc, d_st)
+    torch.cuda.synchronize()
+    lens = d_lens.cpu().numpy().view(np.uint32)
+    icrc = d_icrc.cpu().numpy().view(np.uint32)
+    fr = d_frames.cpu().numpy().reshape(npkts, slot)
+    assert not d_st.cpu().numpy().any()
+    for p, f in enumerate(want):
+        assert lens[p] == len(f), p
+        assert fr[p, : len(f)].tobytes() == f, p
+        assert icrc[p] == O.icrc_of_frame(f), p
+    del d_mr
+    torch.cuda.empty_cache()
