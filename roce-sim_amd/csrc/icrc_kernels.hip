@@ -215,6 +215,21 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
                                             int base, const MainKeys& kk, OutBuf ob);
 
+// A wave issues its next body block's loads at raised priority, so the
+// sequencer sends loads out ahead of other waves' folds and the HBM queue stays
+// full: cfg2 +0.5 % (6012 -> 6042 GiB/s, 3 A/B rounds on each of two boxes;
+// priority 2 the same, cfg3 and the segmentation kernel neutral, also raising
+// it for a packet's first batch measured worse).  0 disables.
+#ifndef RICRC_SETPRIO
+#define RICRC_SETPRIO 3
+#endif
+__device__ __forceinline__ void body_prio_hi() {
+  if constexpr (RICRC_SETPRIO > 0) __builtin_amdgcn_s_setprio(RICRC_SETPRIO);
+}
+__device__ __forceinline__ void body_prio_lo() {
+  if constexpr (RICRC_SETPRIO > 0) __builtin_amdgcn_s_setprio(0);
+}
+
 // Fold, combine, check and emit one packet whose first batch is in `b`.
 template <int LOG2G, bool VERIFY>
 __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, Batch<kUnroll>& b,
@@ -246,8 +261,10 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   for (int bk = 0; bk < nblk; bk += 2) {
     int jn = j0 + bs;
     if (bk + 1 < nblk) {
+      body_prio_hi();
 #pragma unroll
       for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
+      body_prio_lo();
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -256,8 +273,10 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     j0 = jn;
     jn = j0 + U;
     if (bk + 2 < nblk) {
+      body_prio_hi();
 #pragma unroll
       for (int u = 0; u < U; ++u) b.cur[u] = load_body<G>(p, jn + u, gl);
+      body_prio_lo();
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) fold(A, nxt[u], kk);
