@@ -215,11 +215,12 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
                                             int base, const MainKeys& kk, OutBuf ob);
 
-// A wave issues its next body block's loads at raised priority, so the
-// sequencer sends loads out ahead of other waves' folds and the HBM queue stays
-// full: cfg2 +0.5 % (6012 -> 6042 GiB/s, 3 A/B rounds on each of two boxes;
+// A wave issues its next body block's loads (lane-group kernels) or its next
+// batch's prefetch (small-frame kernel) at raised priority, so the sequencer
+// sends loads out ahead of other waves' folds and the HBM queue stays full:
+// cfg2 +0.5 % (6012 -> 6042 GiB/s, 3 A/B rounds on each of two boxes;
 // priority 2 the same, cfg3 and the segmentation kernel neutral, also raising
-// it for a packet's first batch measured worse).  0 disables.
+// it for a packet's first batch measured worse), cfg5 +2.5-12 %.  0 disables.
 #ifndef RICRC_SETPRIO
 #define RICRC_SETPRIO 3
 #endif
@@ -678,7 +679,12 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     for (int t = 0; t < C; ++t)  // chunks past the batch hold a copy of its last one
       *(lds_u32x4*)(uintptr_t)(stage + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1)) = Rg[t];
     __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
+    // the prefetch goes out at raised wave priority: cfg5 +2.5 to +12 % (4326
+    // -> 4437-4855 GiB/s, 6 A/B rounds on two boxes; priority 1-2 +2-3 %;
+    // raising it for the output stores as well measured 12 % slower)
+    body_prio_hi();
     load(bnext, Rg);  // the registers are free again: prefetch the next batch
+    body_prio_lo();
     const uint32_t pb = stage + (uint32_t)lane * S;
     const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
     int ihl;
