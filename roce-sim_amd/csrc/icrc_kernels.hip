@@ -675,14 +675,15 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       return;
     }
 #endif
+    // staging and the prefetch go out at raised wave priority: cfg5 +2.5 to
+    // +12 % (4326 -> 4437-4855 GiB/s, 6 A/B rounds on two boxes; priority 1-2
+    // +2-3 %; raising it for the output stores as well measured 12 % slower,
+    // for the fold at 1-2 +0.3 %, for the staging too +0.5 %, kept)
+    body_prio_hi();
 #pragma unroll
     for (int t = 0; t < C; ++t)  // chunks past the batch hold a copy of its last one
       *(lds_u32x4*)(uintptr_t)(stage + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1)) = Rg[t];
     __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
-    // the prefetch goes out at raised wave priority: cfg5 +2.5 to +12 % (4326
-    // -> 4437-4855 GiB/s, 6 A/B rounds on two boxes; priority 1-2 +2-3 %;
-    // raising it for the output stores as well measured 12 % slower)
-    body_prio_hi();
     load(bnext, Rg);  // the registers are free again: prefetch the next batch
     body_prio_lo();
     const uint32_t pb = stage + (uint32_t)lane * S;
