@@ -60,7 +60,7 @@ extern "C" {
 #define RICRC_EIO (-5)     /* HIP runtime or kernel launch failure          */
 
 /* per-packet status bits (status_out[i]) */
-#define RICRC_PKT_BAD_LEN 0x01       /* len % 4, too short, > 65535, or frame start not 4-byte aligned */
+#define RICRC_PKT_BAD_LEN 0x01       /* len % 4, too short, or > 65535 */
 #define RICRC_PKT_NOT_IPV4 0x02      /* IP version != 4 or IHL < 5 (ICRC = 0)     */
 #define RICRC_PKT_NOT_UDP 0x04       /* IP protocol != 17 (ICRC = 0)              */
 #define RICRC_PKT_LEN_MISMATCH 0x08  /* IP total length != len (ICRC still computed) */

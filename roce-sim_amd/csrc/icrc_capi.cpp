@@ -47,7 +47,21 @@ struct ricrc_ctx {
 
 namespace {
 
-std::once_flag g_prepare_once;
+// Dynamic-LDS limits of every kernel, raised once per device (the attribute
+// is set with that device current) under a lock: contexts on several devices
+// may be created from several threads.
+std::mutex g_prepare_mu;
+std::vector<bool> g_prepared;
+
+hipError_t prepare_device(int device) {
+  std::lock_guard<std::mutex> lk(g_prepare_mu);
+  if ((size_t)device < g_prepared.size() && g_prepared[device]) return hipSuccess;
+  hipError_t e = ricrc::prepare_kernels();
+  if (e != hipSuccess) return e;
+  if ((size_t)device >= g_prepared.size()) g_prepared.resize(device + 1, false);
+  g_prepared[device] = true;
+  return hipSuccess;
+}
 
 int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? RICRC_ENOMEM : RICRC_EIO; }
 
@@ -345,9 +359,7 @@ int ricrc_ctx_create(int device, ricrc_ctx** out) {
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RICRC_ENODEV;
   if (!ricrc::self_test()) return RICRC_EIO;
   HIP_TRY(hipSetDevice(device));
-  hipError_t perr = hipSuccess;
-  std::call_once(g_prepare_once, [&] { perr = ricrc::prepare_kernels(); });
-  if (perr != hipSuccess) return hip_fail(perr);
+  HIP_TRY(prepare_device(device));
 
   ricrc_ctx* c = new (std::nothrow) ricrc_ctx();
   if (!c) return RICRC_ENOMEM;
@@ -474,7 +486,7 @@ int ricrc_compute_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
     for (uint64_t i = d; i < n; i += nctx) {
       offs.push_back(bytes);
       ls.push_back(lens[i]);
-      bytes += (lens[i] + 3u) & ~3u;  // keep every frame dword aligned
+      bytes += ((uint64_t)lens[i] + 3u) & ~(uint64_t)3u;  // keep every frame dword aligned
     }
     const uint32_t m = (uint32_t)offs.size();
     if (m == 0) return;

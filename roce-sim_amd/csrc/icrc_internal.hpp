@@ -43,8 +43,11 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
 hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, int num_cus,
                               hipStream_t stream);
 
-// Raises the dynamic-LDS limit of every kernel instantiation (once per device).
+// Raises the dynamic-LDS limit of every kernel instantiation (ICRC, small
+// frames, segmentation) on the current device; the C ABI calls it once per
+// device (icrc_capi.cpp, prepare_device).
 hipError_t prepare_kernels();
+hipError_t prepare_segment_kernels();
 
 }  // namespace ricrc
 

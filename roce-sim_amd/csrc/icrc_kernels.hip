@@ -75,19 +75,25 @@ struct Pkt {
   int r;              // valid columns in the last iteration (1 .. DPI)
   int jh;             // iterations that may hold dwords k <= 8 (masks, seed, k < 0)
   bool live;          // pkt < n: an output slot exists
-  bool dead;          // nothing to read: outside the batch or unusable length
+  bool dead;          // the main path reads nothing: outside the batch, unusable
+                      // length, or (unless described for the slow path) unaligned
+  bool unal;          // usable frame whose start is not 4-byte aligned: slow path
 };
 
+// `unal_ok`: describe a frame at a non-dword-aligned start for the byte-load
+// slow path (its grid is then anchored at the frame start itself).
 template <int DPI>
 __device__ __forceinline__ Pkt describe(const uint8_t* frames, uint32_t pkt, bool live, uint64_t off,
-                                        uint32_t L) {
+                                        uint32_t L, bool unal_ok = false) {
   Pkt p;
   p.fp = frames + off;
   p.L = L;
   p.pkt = pkt;
   p.live = live;
-  p.dead = !live || L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)p.fp & 3u);
-  p.S = (int)(((uintptr_t)p.fp >> 2) & (DPI - 1));
+  const bool lenbad = L < 44 || (L & 3u) || L > 65535u;
+  p.unal = live && !lenbad && ((uintptr_t)p.fp & 3u) != 0;
+  p.dead = !live || lenbad || (p.unal && !unal_ok);
+  p.S = p.unal ? 0 : (int)(((uintptr_t)p.fp >> 2) & (DPI - 1));
   p.ab = p.fp - 4 * p.S;
   p.n = p.dead ? 1 : (int)((L - 4) >> 2);
   const int E = p.S + p.n;
@@ -106,6 +112,22 @@ __device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
   const int kb = DPI * j + 4 * gl - p.S;
   u32x4 v = {0, 0, 0, 0};
   if (!p.dead && kb + 3 >= 0 && kb < p.n) v = ldg128(p.ab + 16 * (G * j + gl));
+  return v;
+}
+
+// The slow path's chunk of a frame at an unaligned start: byte loads of the
+// covered dwords only (nothing outside the frame is touched).
+__device__ __forceinline__ uint32_t ldg32_bytes(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+template <int G>
+__device__ __forceinline__ u32x4 load_chunk_bytes(const Pkt& p, int j, int gl) {
+  const int kb = 4 * G * j + 4 * gl - p.S;
+  u32x4 v = {0, 0, 0, 0};
+  if (kb + 0 >= 0 && kb + 0 < p.n) v.x = ldg32_bytes(p.fp + 4 * (kb + 0));
+  if (kb + 1 >= 0 && kb + 1 < p.n) v.y = ldg32_bytes(p.fp + 4 * (kb + 1));
+  if (kb + 2 >= 0 && kb + 2 < p.n) v.z = ldg32_bytes(p.fp + 4 * (kb + 2));
+  if (kb + 3 >= 0 && kb + 3 < p.n) v.w = ldg32_bytes(p.fp + 4 * (kb + 3));
   return v;
 }
 
@@ -149,7 +171,8 @@ __device__ __forceinline__ void fix_chunk(u32x4& w, int kb, int kub, int kbb, ui
 
 
 // Recomputation of one packet by its group with the masks of a general IHL
-// (IPv4 options).  Rare path: the main loop applies the IHL-5 masks.
+// (IPv4 options), or of a frame at an unaligned start (byte loads).  Rare
+// path: the main loop applies the IHL-5 masks to dword-aligned frames.
 template <int LOG2G>
 __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, MainKeys kk) {
   constexpr int G = 1 << LOG2G;
@@ -159,7 +182,7 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, M
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < p.J; ++j) {
     const int kb = DPI * j + 4 * gl - p.S;
-    u32x4 w = load_chunk<G>(p, j, gl);
+    u32x4 w = p.unal ? load_chunk_bytes<G>(p, j, gl) : load_chunk<G>(p, j, gl);
     fix_chunk(w, kb, kub, kbb, h0, h2);
     if (j == p.J - 1)
       fold_last(A, w, kb, p.n, kk);
@@ -302,9 +325,14 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
   constexpr int DPI = 4 * G;
   uint32_t B = combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
                                         A.P[3] ^ A.T[3], p.r, gl, base);
-  const uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
-  const uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
-  uint32_t st = p.dead ? kPktBadLen : 0u;
+  uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
+  uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
+  if (p.unal) {  // (per group) frame at an unaligned start: header bytes read directly
+    d0 = ldg32_bytes(p.fp);
+    d2 = ldg32_bytes(p.fp + 8);
+    if (VERIFY) trailer = ldg32_bytes(p.fp + p.L - 4);
+  }
+  uint32_t st = (p.dead && !p.unal) ? kPktBadLen : 0u;
   const int ihl = (int)(d0 & 0xFu);
   if (st == 0) {
     if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
@@ -317,7 +345,9 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
     if (tot != p.L) st |= kPktLenMismatch;
   }
   const bool good = (st & kPktFatal) == 0;
-  if (good && ihl != 5) B = slow_packet<LOG2G>(p, ihl, gl, base, kk);
+  if (good && (ihl != 5 || p.unal))
+    B = slow_packet<LOG2G>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl, gl,
+                           base, kk);
   const uint32_t icrc = good ? ~B : 0u;
   if (p.live && gl == 0) {
     if constexpr (VERIFY) {
@@ -346,6 +376,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   const int tid = threadIdx.x;
 #ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c_start = __builtin_amdgcn_s_memtime();  // shader clock: the ratio is the GFX clock
 #endif
   stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
   __syncthreads();
@@ -392,6 +423,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   if (tid == 0 && a.status_out) {
     ((uint64_t*)a.status_out)[2 * blockIdx.x] = t_start;
     ((uint64_t*)a.status_out)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    ((uint64_t*)a.status_out)[2 * gridDim.x + 2 * blockIdx.x] = c_start;
+    ((uint64_t*)a.status_out)[2 * gridDim.x + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime();
   }
 #endif
 }
@@ -797,6 +830,21 @@ size_t lds_bytes(int log2g, bool ragged) {
   }
 }
 
+template <int C, bool V>
+kernel_fn pick_small(int outs) {
+  switch (outs) {
+    case 0: return icrc_small_kernel<C, V, 0>;
+    case 1: return icrc_small_kernel<C, V, 1>;
+    case 2: return icrc_small_kernel<C, V, 2>;
+    default: return icrc_small_kernel<C, V, 3>;
+  }
+}
+
+kernel_fn select_small(int C, bool verify, int outs) {
+  if (C == 4) return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
+  return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
+}
+
 }  // namespace
 
 void build_table_image(uint32_t* out) {
@@ -815,7 +863,14 @@ hipError_t prepare_kernels() {
                                            (int)lds_bytes(l, r));
         if (e != hipSuccess) return e;
       }
-  return hipSuccess;
+  for (int c : {4, 8})
+    for (int v = 0; v < 2; ++v)
+      for (int o = 0; o < 4; ++o) {
+        hipError_t e = hipFuncSetAttribute((const void*)select_small(c, v, o),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        if (e != hipSuccess) return e;
+      }
+  return prepare_segment_kernels();
 }
 
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
@@ -832,21 +887,6 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   return hipGetLastError();
 }
 
-template <int C, bool V>
-kernel_fn pick_small(int outs) {
-  switch (outs) {
-    case 0: return icrc_small_kernel<C, V, 0>;
-    case 1: return icrc_small_kernel<C, V, 1>;
-    case 2: return icrc_small_kernel<C, V, 2>;
-    default: return icrc_small_kernel<C, V, 3>;
-  }
-}
-
-kernel_fn select_small(int C, bool verify, int outs) {
-  if (C == 4) return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
-  return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
-}
-
 hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   if (a.stride > kSmallMaxStride || (a.stride & 3u) || a.stride == 0) return hipErrorInvalidValue;
@@ -856,18 +896,6 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   const uint32_t slot = 64u * (uint32_t)a.stride;
   const uint32_t nw = min((uint32_t)kSmallMaxWaves, (163840u - kSmallStage) / slot);
   const size_t lds = kSmallStage + (size_t)nw * slot;
-  static const hipError_t prep = [] {
-    for (int c : {4, 8})
-      for (int v = 0; v < 2; ++v)
-        for (int o = 0; o < 4; ++o) {
-          hipError_t e = hipFuncSetAttribute((const void*)select_small(c, v, o),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             163840);
-          if (e != hipSuccess) return e;
-        }
-    return hipSuccess;
-  }();
-  if (prep != hipSuccess) return prep;
   const uint64_t nb = (a.n + 63) / 64;
   uint64_t blocks = (nb + nw - 1) / nw;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;

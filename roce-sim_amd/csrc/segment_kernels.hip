@@ -517,17 +517,20 @@ size_t seg_lds_bytes(int log2g) { return MainKeys::kComb + 4096u * (1 + log2g) +
 
 }  // namespace
 
+hipError_t prepare_segment_kernels() {
+  for (int l = 1; l <= 4; ++l) {
+    hipError_t e = hipFuncSetAttribute((const void*)select_segment(l),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)seg_lds_bytes(l));
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_segment(const SegArgs& a, int log2g, int num_cus, hipStream_t stream) {
   if (a.npkts == 0) return hipSuccess;
   seg_fn k = select_segment(log2g);
   if (!k) return hipErrorInvalidValue;
-  static bool prepared[5] = {false, false, false, false, false};
-  if (!prepared[log2g]) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)seg_lds_bytes(log2g));
-    if (e != hipSuccess) return e;
-    prepared[log2g] = true;
-  }
   if (a.nwr) {
     const uint32_t mb = a.nwr < 8192u ? a.nwr : 8192u;
     hipLaunchKernelGGL(seg_map_kernel, dim3(mb), dim3(256), 0, stream, a);

@@ -14,6 +14,7 @@ from .engine import (  # noqa: F401
     IcrcUnavailable,
     compute_batch_multi,
     load_library,
+    pack_aligned,
     pack_icrc,
     seg_wrs,
     segment_plan,

@@ -191,6 +191,32 @@ def _ptr(a) -> int | None:
     return int(a)
 
 
+def _descriptors(offsets, lens) -> tuple[np.ndarray, np.ndarray]:
+    """(offsets u64, lens u32) of a ragged batch; one entry per frame in each."""
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ls = np.ascontiguousarray(lens, dtype=np.uint32)
+    if offs.ndim != 1 or ls.ndim != 1 or offs.size != ls.size:
+        raise ValueError(f"offsets ({offs.size}) and lens ({ls.size}) must be 1-D and the same "
+                         "length")
+    return offs, ls
+
+
+def pack_aligned(frames) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Pack byte strings into one buffer with every frame starting on a 4-byte
+    boundary (the kernels' fast path; a frame at an unaligned offset takes a
+    slow path).  A datagram of odd length therefore cannot shift the frames
+    after it.  Returns (buffer, offsets, lens)."""
+    lens = np.fromiter((len(f) for f in frames), dtype=np.uint32, count=len(frames))
+    slots = (lens.astype(np.uint64) + 3) & ~np.uint64(3)
+    offs = np.zeros(len(frames), np.uint64)
+    if len(frames) > 1:
+        offs[1:] = np.cumsum(slots[:-1])
+    buf = np.zeros(int(slots.sum()), np.uint8)
+    for f, o in zip(frames, offs):
+        buf[int(o):int(o) + len(f)] = np.frombuffer(f, np.uint8)
+    return buf, offs, lens
+
+
 def _u8(a) -> np.ndarray:
     if isinstance(a, (bytes, bytearray, memoryview)):
         return np.frombuffer(a, dtype=np.uint8)
@@ -265,8 +291,7 @@ class IcrcEngine:
 
     def compute_batch(self, frames, offsets, lens):
         f = _u8(frames)
-        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
-        ls = np.ascontiguousarray(lens, dtype=np.uint32)
+        offs, ls = _descriptors(offsets, lens)
         n = offs.size
         out = np.zeros(n, np.uint32)
         st = np.zeros(n, np.uint8)
@@ -276,8 +301,7 @@ class IcrcEngine:
 
     def verify_batch(self, frames, offsets, lens):
         f = _u8(frames)
-        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
-        ls = np.ascontiguousarray(lens, dtype=np.uint32)
+        offs, ls = _descriptors(offsets, lens)
         n = offs.size
         ok = np.zeros(n, np.uint8)
         out = np.zeros(n, np.uint32)
@@ -381,8 +405,7 @@ def compute_batch_multi(engines: list[IcrcEngine], frames, offsets, lens):
     """Round-robin split over several GPUs (packet i -> engines[i % len])."""
     lib = load_library()
     f = _u8(frames)
-    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
-    ls = np.ascontiguousarray(lens, dtype=np.uint32)
+    offs, ls = _descriptors(offsets, lens)
     n = offs.size
     arr = (_vp * len(engines))(*[e.ctx.value for e in engines])
     out = np.zeros(n, np.uint32)

@@ -32,6 +32,8 @@ from typing import Optional
 
 import numpy as np
 
+from .engine import pack_aligned
+
 ROCE_PORT = 4791  # src/roce_enum.py:14
 
 _transports = {"RC": 0x00, "UC": 0x20, "RD": 0x40, "UD": 0x60, "CNP": 0x80, "XRC": 0xA0}
@@ -541,15 +543,9 @@ def emit_batch(pkts: list[Packet]) -> list[bytes]:
         frames.append(placeholder.build())
         need.append(i)
     if need:
-        offs = np.zeros(len(need), np.uint64)
-        lens = np.zeros(len(need), np.uint32)
-        parts, pos = [], 0
-        for j, i in enumerate(need):
-            offs[j] = pos
-            lens[j] = len(frames[i])
-            parts.append(frames[i])
-            pos += len(frames[i])
-        icrc, _ = get_engine().compute_batch(np.frombuffer(b"".join(parts), np.uint8), offs, lens)
+        # frames at dword-aligned offsets, whatever their lengths
+        buf, offs, lens = pack_aligned([frames[i] for i in need])
+        icrc, _ = get_engine().compute_batch(buf, offs, lens)
         for j, i in enumerate(need):
             f = bytearray(frames[i])
             f[-4:] = BTH.pack_icrc(int(icrc[j]) ^ pkts[i][BTH].icrc_fault)
@@ -568,11 +564,10 @@ def emit_batch(pkts: list[Packet]) -> list[bytes]:
 def verify_frames(frames: list[bytes]) -> np.ndarray:
     """Receive-side ICRC check over full IPv4 frames (new behaviour: the
     reference never verifies), one GPU call."""
-    offs = np.zeros(len(frames), np.uint64)
-    lens = np.array([len(f) for f in frames], np.uint32)
-    if len(frames) > 1:
-        offs[1:] = np.cumsum(lens[:-1])
-    ok, _, _ = get_engine().verify_batch(np.frombuffer(b"".join(frames), np.uint8), offs, lens)
+    # dword-aligned offsets: a datagram of odd length (a stray or truncated
+    # UDP packet) must not shift the frames after it
+    buf, offs, lens = pack_aligned(frames)
+    ok, _, _ = get_engine().verify_batch(buf, offs, lens)
     return ok
 
 

@@ -71,3 +71,26 @@ def test_header_is_plain_c_and_links(tmp_path):
         pytest.skip("the run leg is for GPU-less hosts (device 0 would be initialised)")
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
     assert out.startswith("abi 2 ok: 4 packets, slot 4352"), out
+
+
+def test_descriptor_arrays_must_match():
+    """offsets and lens of a ragged batch must have one entry per frame each
+    (a shorter lens array would make the C library read past its end)."""
+    import numpy as np
+    offs, ls = E._descriptors([0, 64, 128], [44, 44, 44])
+    assert offs.dtype == np.uint64 and ls.dtype == np.uint32
+    with pytest.raises(ValueError):
+        E._descriptors([0, 64, 128], [44, 44])
+    with pytest.raises(ValueError):
+        E._descriptors(np.zeros((2, 2)), np.zeros((2, 2)))
+
+
+def test_pack_aligned_keeps_every_frame_dword_aligned():
+    import numpy as np
+    frames = [b"\x01" * 47, b"\x02" * 3, b"\x03" * 44, b"", b"\x04" * 5]
+    buf, offs, lens = E.pack_aligned(frames)
+    assert list(lens) == [47, 3, 44, 0, 5]
+    assert list(offs) == [0, 48, 52, 96, 96]
+    assert (offs % 4 == 0).all() and buf.size == 104
+    for f, o in zip(frames, offs):
+        assert buf[int(o):int(o) + len(f)].tobytes() == f

@@ -82,3 +82,30 @@ def test_recv_datagrams_drops_bad_icrc(engine):
     assert got[0][R.Raw].load == bytes([0]) * 64
     got, dropped = R.recv_datagrams(frames, qpn=0x31)
     assert [b.psn for b in got] == [1, 3, 5, 7, 9]
+
+
+def test_odd_length_datagram_does_not_shift_the_batch(engine):
+    """A stray datagram whose length is not a multiple of 4 (truncated UDP
+    packet) in the middle of a receive batch: it fails, and every valid frame
+    after it still verifies and is delivered (frames are packed at dword-aligned
+    offsets); emit_batch with an odd-length frame in the batch still writes the
+    right ICRC into the frames after it."""
+    R.set_engine(engine)
+    pkts = [R.l3_packet(R.BTH(opcode=0x01, psn=i, dqpn=0x30) / R.Raw(load=bytes([i]) * 64),
+                        dst="10.0.0.2", sport=7, src="10.0.0.1") for i in range(8)]
+    frames = R.emit_batch(pkts)
+    for cut in (1, 2, 3):
+        stray = frames[0][:-cut]  # length not a multiple of 4
+        batch = frames[:3] + [stray] + frames[3:]
+        ok = R.verify_frames(batch)
+        assert list(ok) == [True] * 3 + [False] + [True] * 5
+        got, dropped = R.recv_datagrams(batch)
+        assert dropped == [3] and [b.psn for b in got] == list(range(8))
+    # emit side: a BTH/Raw build without padding gives an odd-length frame
+    raw = R.IP(src="10.0.0.1", dst="10.0.0.2") / R.UDP(dport=4791, sport=7) / \
+        R.BTH(opcode=0x04, psn=99, dqpn=0x30) / R.Raw(load=b"\x01\x02\x03")
+    mixed = R.emit_batch(pkts[:2] + [raw] + pkts[2:])
+    assert len(mixed[2]) % 4 == 3
+    assert mixed[:2] + mixed[3:] == frames
+    for f in frames:
+        assert o.verify_frame(f)

@@ -221,27 +221,93 @@ def test_maximum_length_frames(engine):
     engine.set_lanes(0)
 
 
-def test_misaligned_frame_is_flagged(engine):
-    """A frame whose start is not 4-byte aligned is not read: ICRC 0 and
-    PKT_BAD_LEN (the kernels walk dword-aligned chunks); its neighbours are
-    unaffected, on the staged small-call path and on a large batch."""
-    good = o.build_frame("1.2.3.4", "5.6.7.8", 9, dict(opcode=0x04, psn=7),
-                         payload=bytes(range(256)))
-    for reps in (1, 3000):  # 3000 frames: past the pinned staging block
-        buf = np.zeros((len(good) + 8) * (reps + 1) + 8, np.uint8)
-        offs, lens = [], []
-        pos = 0
-        for i in range(reps):
-            buf[pos:pos + len(good)] = np.frombuffer(good, np.uint8)
-            offs.append(pos)
-            pos += len(good) + 4
-        odd = pos + 2
-        buf[odd:odd + len(good)] = np.frombuffer(good, np.uint8)
-        offs.append(odd)
-        lens = np.full(reps + 1, len(good), np.uint32)
-        got, st = engine.compute_batch(buf, np.array(offs, np.uint64), lens)
-        assert (got[:-1] == o.icrc_of_frame(good)).all() and (st[:-1] == 0).all()
-        assert got[-1] == 0 and st[-1] & PKT_BAD_LEN
+@pytest.mark.parametrize("lanes", [0, 1, 8, 64])
+def test_misaligned_frames(engine, lanes):
+    """Frames whose start is not 4-byte aligned get their real ICRC, like the
+    reference's zlib.crc32 wherever the bytes sit (byte-load slow path), in
+    compute and verify, on the staged small-call path and on a large batch;
+    the aligned neighbours are unaffected and the multi-GPU entry point (which
+    realigns while gathering) agrees."""
+    from roce_icrc import compute_batch_multi
+    rng = np.random.default_rng(3 + lanes)
+    frames = [o.build_frame("1.2.3.4", "5.6.7.8", 9, dict(opcode=0x04, psn=i),
+                            payload=rng.integers(0, 256, int(rng.integers(0, 1100)),
+                                                 dtype=np.uint8).tobytes())
+              for i in range(40)]
+    frames[7] = o.build_frame("1.2.3.4", "5.6.7.8", 9, dict(opcode=0x04, psn=7))  # 44 B minimum
+    want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
+    engine.set_lanes(lanes)
+    try:
+        for reps in (1, 80):  # 80 x 40 frames: past the pinned staging block
+            fs = frames * reps
+            buf = np.zeros(sum(len(f) + 8 for f in fs) + 8, np.uint8)
+            offs, pos = [], 0
+            for i, f in enumerate(fs):
+                pos += i % 4  # every byte misalignment, in turn
+                buf[pos:pos + len(f)] = np.frombuffer(f, np.uint8)
+                offs.append(pos)
+                pos += len(f)
+            offs = np.array(offs, np.uint64)
+            lens = np.array([len(f) for f in fs], np.uint32)
+            assert len({int(x) % 4 for x in offs}) == 4
+            got, st = engine.compute_batch(buf, offs, lens)
+            np.testing.assert_array_equal(got, np.tile(want, reps))
+            assert (st == 0).all()
+            got_m, st_m = compute_batch_multi([engine, engine], buf, offs, lens)
+            np.testing.assert_array_equal(got_m, got)
+            np.testing.assert_array_equal(st_m, st)
+            for i, f in enumerate(fs):
+                e = int(offs[i]) + len(f)
+                buf[e - 4:e] = np.frombuffer(int(want[i % 40]).to_bytes(4, "little"), np.uint8)
+            bad = [5, 6, 22, 23]  # one per misalignment: a payload bit flip must fail
+            for i in bad:
+                buf[int(offs[i]) + 40] ^= 0x10
+            ok, got2, st2 = engine.verify_batch(buf, offs, lens)
+            expect = np.ones(len(fs), bool)
+            expect[bad] = False
+            np.testing.assert_array_equal(ok, expect)
+            assert (st2[bad] & PKT_ICRC_MISMATCH).all()
+    finally:
+        engine.set_lanes(0)
+
+
+def test_misaligned_frames_device_resident(engine):
+    """The device-resident ragged entry points and a strided batch whose
+    stride is not a multiple of 4 (every other frame unaligned)."""
+    import torch
+    rng = np.random.default_rng(17)
+    frames = [o.build_frame("10.0.0.1", "10.0.0.2", 3, dict(opcode=0x07, psn=i),
+                            payload=rng.integers(0, 256, 4 * int(rng.integers(0, 300)),
+                                                 dtype=np.uint8).tobytes())
+              for i in range(3000)]
+    want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
+    buf = np.zeros(sum(len(f) + 3 for f in frames), np.uint8)
+    offs, pos = [], 0
+    for i, f in enumerate(frames):
+        pos += i % 4
+        buf[pos:pos + len(f)] = np.frombuffer(f, np.uint8)
+        offs.append(pos)
+        pos += len(f)
+    lens = np.array([len(f) for f in frames], np.uint32)
+    d_buf = torch.from_numpy(buf).cuda()
+    d_offs = torch.from_numpy(np.array(offs, np.int64)).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.zeros(len(frames), dtype=torch.int32, device="cuda")
+    st = torch.zeros(len(frames), dtype=torch.uint8, device="cuda")
+    engine.compute_batch_dev(d_buf, d_offs, d_lens, len(frames), out, st)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert (st.cpu().numpy() == 0).all()
+    # strided: 2 + 4140-B stride, so frame i starts at 2 i (mod 4)
+    sb, stride, flen = synth.uniform_frames(64, 4096, seed=5)
+    f2 = [sb[i * stride:i * stride + flen].tobytes() for i in range(64)]
+    s2 = flen + 2
+    buf2 = np.zeros(64 * s2, np.uint8)
+    for i, f in enumerate(f2):
+        buf2[i * s2:i * s2 + flen] = np.frombuffer(f, np.uint8)
+    got, st2 = engine.compute_strided(buf2, s2, flen, 64)
+    np.testing.assert_array_equal(got, [o.icrc_of_frame(f) for f in f2])
+    assert (st2 == 0).all()
 
 
 def test_mask_invariance_and_sensitivity(engine):
