@@ -378,15 +378,17 @@ class Segment:
                 "lens_ok": bool((self.d_lens > 0).all())}
 
 
-CEIL_MIN_S = 0.08  # the ceiling series runs back to back for at least this long
+CEIL_MIN_S = float(os.environ.get("ROCE_ICRC_CEIL_S", "0.08"))  # ceiling series length (s)
 
 
-def measure_ceiling(torch, eng, W, stream, sp, dev):
+def enqueue_ceiling(torch, eng, W, stream, sp, dev):
     """Measured HBM ceiling on the same buffers: STREAM read of the frame
     buffer (16-B nt loads, one workgroup per CU sweeping a contiguous chunk,
     the ICRC kernels' geometry), or for segmentation the STREAM copy of the MR
-    into the frame buffer (read + write bytes).  Median over a back-to-back
-    series of >= CEIL_MIN_S."""
+    into the frame buffer (read + write bytes): a back-to-back series of
+    >= CEIL_MIN_S, ENQUEUED without a final synchronisation so the warm-up
+    steps follow it with no idle gap (see main()).  Returns a function that,
+    after the stream has been synchronised, gives (key, GB/s median, times)."""
     if isinstance(W, Segment):
         nb = W.mr.size // 16 * 16
         key, nbytes = "stream_copy_GBps", 2 * nb
@@ -412,9 +414,11 @@ def measure_ceiling(torch, eng, W, stream, sp, dev):
         a.record(stream)
         launch()
         b.record(stream)
-    torch.cuda.synchronize(dev)
-    ts = [a.elapsed_time(b) * 1e-3 for a, b in evs]
-    return key, nbytes / float(np.median(ts)) / 1e9, ts
+
+    def result():
+        ts = [a.elapsed_time(b) * 1e-3 for a, b in evs]
+        return key, nbytes / float(np.median(ts)) / 1e9, ts
+    return result
 
 
 def main():
@@ -448,14 +452,19 @@ def main():
     sp = stream.cuda_stream
 
     # The measured HBM ceiling (STREAM read of the same frame buffer, or the
-    # STREAM copy for segmentation) runs FIRST, right before the warm-up: from
-    # an idle GPU the first ~25 launches of the ICRC kernels run up to 25 %
-    # slower while the chip's power management settles (measured per launch,
-    # profiles/r02_transient.txt), whereas coming straight from another
-    # HBM-saturating kernel they do not.  The timed steps are unchanged.
-    ceil_key, ceil_gbps, ceil_ts = measure_ceiling(torch, eng, W, stream, sp, dev)
+    # STREAM copy for segmentation) is enqueued FIRST and the warm-up steps
+    # right behind it, with no synchronisation in between: when the ICRC
+    # kernels start on a GPU that has been idle for more than a few ms, the
+    # chip's power management pulls the shader clock from ~2.1 GHz down to
+    # ~1.1 GHz for launches 3-10 and takes ~50 launches to recover (up to 25 %
+    # slower launches); coming straight from another HBM-saturating kernel
+    # they do not dip (measured: profiles/r02_transient.txt).  The timed steps
+    # are unchanged.
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
     wev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.warmup)]
+    ceiling = enqueue_ceiling(torch, eng, W, stream, sp, dev)
     for a, b in wev:
         a.record(stream)
         W.step(sp)
@@ -464,8 +473,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for a, b in evs:
         a.record(stream)
@@ -476,9 +483,10 @@ def main():
     if world > 1:
         dist.barrier()
     kern_s = [a.elapsed_time(b) * 1e-3 for a, b in evs]
+    ceil_key, ceil_gbps, ceil_ts = ceiling()
     if os.environ.get("ROCE_ICRC_BENCH_TRACE"):  # per-launch times (us) to stderr
         us = lambda xs: [round(x * 1e6) for x in xs]  # noqa: E731
-        print(f"[trace] rank {rank} ceiling {us(ceil_ts)}\n[trace] warmup "
+        print(f"[trace] rank {rank} ceiling n={len(ceil_ts)} {us(ceil_ts)}\n[trace] warmup "
               f"{us([a.elapsed_time(b) * 1e-3 for a, b in wev])}\n[trace] timed {us(kern_s)}",
               file=sys.stderr, flush=True)
     t = torch.tensor([t_local], dtype=torch.float64)

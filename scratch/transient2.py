@@ -50,6 +50,8 @@ def series(fn, k):
 pre = []
 if mode == "stream":
     pre = series(stream, 100)
+elif mode == "stream20":
+    pre = series(stream, 20)
 elif mode == "stream400":
     pre = series(stream, 400)
 elif mode == "icrc":
