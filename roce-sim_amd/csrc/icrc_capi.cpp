@@ -23,7 +23,6 @@ struct ricrc_ctx {
   int device = -1;
   int num_cus = 0;
   int lanes = 0;  // 0 = automatic
-  int chunks_lv = -1;  // log2 of 16-byte chunks per lane per iteration (-1 = automatic)
   hipStream_t stream = nullptr;
   uint32_t* d_tables = nullptr;
   // scratch for the host-buffer entry points
@@ -109,12 +108,6 @@ int ragged_log2g(const ricrc_ctx* c, uint32_t mean) {
 
 hipStream_t pick_stream(const ricrc_ctx*, void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Chunks per lane for G = 2^log2g lanes per packet (only instantiated pairs).
-int pick_lv(const ricrc_ctx* c, int log2g) {
-  const int lv = c->chunks_lv >= 0 ? c->chunks_lv : 0;
-  return ricrc::has_chunks(log2g, lv) ? lv : 0;
-}
-
 int ensure_frames(ricrc_ctx* c, size_t bytes) {
   if (bytes <= c->frames_cap) return RICRC_OK;
   if (c->d_frames) (void)hipFree(c->d_frames);
@@ -174,7 +167,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0)
     HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
   else
-    HIP_TRY(ricrc::launch_icrc(a, log2g, pick_lv(c, log2g), ragged, verify, c->num_cus, s));
+    HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
   return RICRC_OK;
 }
 
@@ -372,10 +365,6 @@ int ricrc_ctx_create(int device, ricrc_ctx** out) {
   if (!c) return RICRC_ENOMEM;
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
-  if (const char* v = std::getenv("ROCE_ICRC_CHUNKS")) {  // exploration override (1, 2, 4)
-    const int n = std::atoi(v);
-    c->chunks_lv = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : -1;
-  }
   std::vector<uint32_t> img(ricrc::kTableWords);
   ricrc::build_table_image(img.data());
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

@@ -232,100 +232,17 @@ __device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n,
   }
 }
 
-// ---------------------------------------------------------------------------
-// V chunks per lane: a lane holds CPL = 4 V grid columns per iteration (V
-// consecutive 16-byte chunks), so a group of G lanes still reads an aligned
-// 16 G V-byte run while fewer lanes share the per-packet work (describe, head
-// fix-ups, rotation, combine).  V = 1 is the layout above.
-template <int V>
-struct ColV {
-  uint32_t P[4 * V], T[4 * V];
-};
-
-template <int V, class K>
-__device__ __forceinline__ void foldV(ColV<V>& c, const u32x4 (&w)[V], const K& k) {
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    absorb(c.P[4 * v + 0], c.T[4 * v + 0], w[v].x, k);
-    absorb(c.P[4 * v + 1], c.T[4 * v + 1], w[v].y, k);
-    absorb(c.P[4 * v + 2], c.T[4 * v + 2], w[v].z, k);
-    absorb(c.P[4 * v + 3], c.T[4 * v + 3], w[v].w, k);
-  }
-}
-
-// The packet's last iteration: lane columns t with kb + t >= n keep their register.
-template <int V, class K>
-__device__ __forceinline__ void fold_lastV(ColV<V>& c, const u32x4 (&w)[V], int kb, int n,
-                                           const K& k) {
-  ColV<V> f = c;
-  foldV<V>(f, w, k);
-#pragma unroll
-  for (int t = 0; t < 4 * V; ++t) {
-    c.P[t] = (kb + t < n) ? f.P[t] : c.P[t];
-    c.T[t] = (kb + t < n) ? f.T[t] : c.T[t];
-  }
-}
-
-// combine() for CPL = 4 V columns per lane: rotate the group's columns by r
-// (an in-lane barrel rotation by r mod CPL, then one ds_bpermute per column
-// from lane gl + r / CPL or the one after it), then R = sum_c' Mul(-32 c')(V_c')
-// as CPL - 1 in-lane Horner steps with Mul(-32) and log2 G butterfly levels
-// with Mul(-32 CPL 2^l) (combine slot 1 + l).
-template <int LOG2G, int V, class K>
-__device__ __forceinline__ uint32_t combineV(const ColV<V>& A, int r, int gl, int base) {
-  constexpr int G = 1 << LOG2G;
-  constexpr int CPL = 4 * V;
-  constexpr int LC = V == 1 ? 2 : V == 2 ? 3 : V == 4 ? 4 : 5;
-  static_assert((1 << LC) == CPL, "V must be 1, 2, 4 or 8");
-  constexpr int DPI = G * CPL;
-  const int rr = r & (DPI - 1);
-  const int q = rr >> LC, m = rr & (CPL - 1);
-  uint32_t v[CPL];
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) v[t] = A.P[t] ^ A.T[t];
-#pragma unroll
-  for (int b = 0; b < LC; ++b) {  // v[t] <- v[(t + m) mod CPL]
-    uint32_t nv[CPL];
-    const bool on = (m >> b) & 1;
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) nv[t] = on ? v[(t + (1 << b)) & (CPL - 1)] : v[t];
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) v[t] = nv[t];
-  }
-  if constexpr (G > 1) {
-    const int s0 = base + ((gl + q) & (G - 1));
-    const int s1 = base + ((gl + q + 1) & (G - 1));
-#pragma unroll
-    for (int t = 0; t < CPL; ++t) v[t] = (uint32_t)__shfl((int)v[t], t + m >= CPL ? s1 : s0, 64);
-  }
-  uint32_t B = v[CPL - 1];
-#pragma unroll
-  for (int t = CPL - 2; t >= 0; --t) B = mul_comb(B, K::kComb) ^ v[t];
-#pragma unroll
-  for (int l = 0; l < LOG2G; ++l) {
-    const uint32_t mm = mul_comb(B, K::kComb + 4096u * (1 + l));
-    const uint32_t t = ((gl >> l) & 1) ? mm : B;
-    B = t ^ (uint32_t)__shfl_xor((int)t, 1 << l, 64);
-  }
-  return B;
-}
-
 // LDS address of the IHL-5 fix-up table (after the combine sets).
 template <int LOG2G, class K>
 constexpr uint32_t kFixLut = K::kComb + 4096u * (1 + LOG2G);
 
-// LDS staging of the folding tables (every lane-group kernel, once per
-// workgroup): the main set Mul(128 G V) (index LOG2G + LV, V = 2^LV), combine
-// slot 0 = Mul(-32) and slot 1 + l = Mul(-128 V 2^l) (image set 1 + l + LV).
-template <int LOG2G, int THREADS, class K, int LV = 0>
+// LDS staging of the folding tables (every lane-group kernel, once per workgroup).
+template <int LOG2G, int THREADS, class K>
 __device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
   constexpr int NCOMB = 1 + LOG2G;
-  K::template stage<THREADS>(tables + (LOG2G + LV) * 1024, tid);
+  K::template stage<THREADS>(tables + LOG2G * 1024, tid);
   const uint32_t* gc = tables + kNumMainSets * 1024;
-  for (int i = tid; i < NCOMB * 1024; i += THREADS) {
-    const int slot = i >> 10;
-    lds_wr(K::kComb + 4u * i, gc[(slot == 0 ? 0 : slot + LV) * 1024 + (i & 1023)]);
-  }
+  for (int i = tid; i < NCOMB * 1024; i += THREADS) lds_wr(K::kComb + 4u * i, gc[i]);
   if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
     const int k = tid - 3;
     const uint32_t lut = kFixLut<LOG2G, K>;

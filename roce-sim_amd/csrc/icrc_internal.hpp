@@ -30,12 +30,9 @@ struct IcrcArgs {
 // Builds the table image on the host (kTableWords words).
 void build_table_image(uint32_t* out);
 
-// Enqueues the lane-group ICRC kernel with G = 2^log2g lanes per packet and
-// V = 2^lv 16-byte chunks per lane per iteration; returns a hipError_t.
-hipError_t launch_icrc(const IcrcArgs& a, int log2g, int lv, bool ragged, bool verify, int num_cus,
+// Enqueues the ICRC kernel; returns a hipError_t.
+hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
                        hipStream_t stream);
-// Whether the (G, V) pair is instantiated.
-bool has_chunks(int log2g, int lv);
 
 // Strided frames of at most kSmallMaxStride bytes (stride a multiple of 4):
 // the lane-per-packet kernel with LDS-staged, coalesced loads.

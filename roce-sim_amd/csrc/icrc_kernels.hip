@@ -103,53 +103,38 @@ __device__ __forceinline__ Pkt describe(const uint8_t* frames, uint32_t pkt, boo
   return p;
 }
 
-// Lane chunk geometry: in iteration j lane gl of a group holds the grid
-// dwords DPI j + CPL gl + [0, CPL), CPL = 4 V, as V consecutive 16-byte
-// chunks; chunk v starts at frame dword kb = DPI j + CPL gl + 4 v - S.
-template <int V>
-constexpr int kLog2Cpl = V == 1 ? 2 : V == 2 ? 3 : V == 4 ? 4 : 5;
-// body iterations per block (16-byte loads in flight per lane: U V = kUnroll)
-template <int V>
-constexpr int kBodyU = kUnroll / V > 0 ? kUnroll / V : 1;
-
-// The lane's chunks of iteration j; chunks with no covered dword are not
-// loaded.  An aligned 4 DPI-byte block never crosses a page, so the bytes
+// The lane's 16-byte chunk of iteration j; chunks with no covered dword are
+// not loaded.  An aligned 4 DPI-byte block never crosses a page, so the bytes
 // around the frame that share its blocks are always mapped.
-template <int G, int V>
-__device__ __forceinline__ void load_chunk(u32x4 (&w)[V], const Pkt& p, int j, int gl) {
-  constexpr int DPI = 4 * G * V;
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    const int kb = DPI * j + 4 * (V * gl + v) - p.S;
-    w[v] = u32x4{0, 0, 0, 0};
-    if (!p.dead && kb + 3 >= 0 && kb < p.n) w[v] = ldg128(p.ab + 16 * (G * V * j + V * gl + v));
-  }
+template <int G>
+__device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
+  constexpr int DPI = 4 * G;
+  const int kb = DPI * j + 4 * gl - p.S;
+  u32x4 v = {0, 0, 0, 0};
+  if (!p.dead && kb + 3 >= 0 && kb < p.n) v = ldg128(p.ab + 16 * (G * j + gl));
+  return v;
 }
 
-// The slow path's chunks of a frame at an unaligned start: byte loads of the
+// The slow path's chunk of a frame at an unaligned start: byte loads of the
 // covered dwords only (nothing outside the frame is touched).
 __device__ __forceinline__ uint32_t ldg32_bytes(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
-template <int G, int V>
-__device__ __forceinline__ void load_chunk_bytes(u32x4 (&w)[V], const Pkt& p, int j, int gl) {
-  constexpr int DPI = 4 * G * V;
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    const int kb = DPI * j + 4 * (V * gl + v) - p.S;
-    w[v] = u32x4{0, 0, 0, 0};
-    if (kb + 0 >= 0 && kb + 0 < p.n) w[v].x = ldg32_bytes(p.fp + 4 * (kb + 0));
-    if (kb + 1 >= 0 && kb + 1 < p.n) w[v].y = ldg32_bytes(p.fp + 4 * (kb + 1));
-    if (kb + 2 >= 0 && kb + 2 < p.n) w[v].z = ldg32_bytes(p.fp + 4 * (kb + 2));
-    if (kb + 3 >= 0 && kb + 3 < p.n) w[v].w = ldg32_bytes(p.fp + 4 * (kb + 3));
-  }
+template <int G>
+__device__ __forceinline__ u32x4 load_chunk_bytes(const Pkt& p, int j, int gl) {
+  const int kb = 4 * G * j + 4 * gl - p.S;
+  u32x4 v = {0, 0, 0, 0};
+  if (kb + 0 >= 0 && kb + 0 < p.n) v.x = ldg32_bytes(p.fp + 4 * (kb + 0));
+  if (kb + 1 >= 0 && kb + 1 < p.n) v.y = ldg32_bytes(p.fp + 4 * (kb + 1));
+  if (kb + 2 >= 0 && kb + 2 < p.n) v.z = ldg32_bytes(p.fp + 4 * (kb + 2));
+  if (kb + 3 >= 0 && kb + 3 < p.n) v.w = ldg32_bytes(p.fp + 4 * (kb + 3));
+  return v;
 }
 
 // Body iterations (jh <= j < J-1) lie wholly inside the frame: no predicate.
-template <int G, int V>
-__device__ __forceinline__ void load_body(u32x4 (&w)[V], const Pkt& p, int j, int gl) {
-#pragma unroll
-  for (int v = 0; v < V; ++v) w[v] = ldg128(p.ab + 16 * (G * V * j + V * gl + v));
+template <int G>
+__device__ __forceinline__ u32x4 load_body(const Pkt& p, int j, int gl) {
+  return ldg128(p.ab + 16 * (G * j + gl));
 }
 
 
@@ -188,68 +173,54 @@ __device__ __forceinline__ void fix_chunk(u32x4& w, int kb, int kub, int kbb, ui
 // Recomputation of one packet by its group with the masks of a general IHL
 // (IPv4 options), or of a frame at an unaligned start (byte loads).  Rare
 // path: the main loop applies the IHL-5 masks to dword-aligned frames.
-template <int LOG2G, int V>
+template <int LOG2G>
 __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, MainKeys kk) {
   constexpr int G = 1 << LOG2G;
-  constexpr int CPL = 4 * V;
-  constexpr int DPI = G * CPL;
+  constexpr int DPI = 4 * G;
   const int kub = ihl + 1, kbb = ihl + 3;
-  ColV<V> A;
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) A.P[t] = A.T[t] = 0;
+  Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < p.J; ++j) {
-    const int kb = DPI * j + CPL * gl - p.S;
-    u32x4 w[V];
-    if (p.unal)
-      load_chunk_bytes<G, V>(w, p, j, gl);
-    else
-      load_chunk<G, V>(w, p, j, gl);
-#pragma unroll
-    for (int v = 0; v < V; ++v) fix_chunk(w[v], kb + 4 * v, kub, kbb, h0, h2);
+    const int kb = DPI * j + 4 * gl - p.S;
+    u32x4 w = p.unal ? load_chunk_bytes<G>(p, j, gl) : load_chunk<G>(p, j, gl);
+    fix_chunk(w, kb, kub, kbb, h0, h2);
     if (j == p.J - 1)
-      fold_lastV<V>(A, w, kb, p.n, kk);
+      fold_last(A, w, kb, p.n, kk);
     else
-      foldV<V>(A, w, kk);
+      fold(A, w, kk);
   }
-  return combineV<LOG2G, V, MainKeys>(A, p.r, gl, base);
+  return combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                  A.P[3] ^ A.T[3], p.r, gl, base);
 }
 
 
 // A packet's first batch of loads: head chunks, the first body block and the
-// last chunk (plus the trailer in verify mode).
-template <int U, int V>
+// last chunk (plus the trailer in verify mode).  Issued one packet set ahead
+// so small packets do not wait a full HBM round trip per set.
+template <int U>
 struct Batch {
-  u32x4 wh0[V], wh1[V], wl[V];
-  u32x4 cur[U][V];
+  u32x4 wh0, wh1, wl;
+  u32x4 cur[U];
   uint32_t trailer;
 };
 
-template <int LOG2G, int V, bool VERIFY>
-__device__ __forceinline__ Batch<kBodyU<V>, V> issue_packet(const Pkt& p, int gl) {
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
   constexpr int G = 1 << LOG2G;
-  constexpr int U = kBodyU<V>;
-  Batch<U, V> b;
+  constexpr int U = kUnroll;
+  Batch<U> b;
   const int JL = p.J - 1;
   const int jhh = min(p.jh, JL);
   const int nbody = JL - jhh;
   const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
   b.trailer = 0;
   if (VERIFY && !p.dead && gl == 0) b.trailer = ldg32(p.fp + p.L - 4);
+  b.wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
+  b.wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
 #pragma unroll
-  for (int v = 0; v < V; ++v) b.wh0[v] = b.wh1[v] = u32x4{0, 0, 0, 0};
-  if (jhh > 0) load_chunk<G, V>(b.wh0, p, 0, gl);
-  if (jhh > 1) load_chunk<G, V>(b.wh1, p, 1, gl);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    if (u < first) {
-      load_body<G, V>(b.cur[u], p, jhh + u, gl);
-    } else {
-#pragma unroll
-      for (int v = 0; v < V; ++v) b.cur[u][v] = u32x4{0, 0, 0, 0};
-    }
-  }
-  load_chunk<G, V>(b.wl, p, JL, gl);
+  for (int u = 0; u < U; ++u)
+    b.cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
+  b.wl = load_chunk<G>(p, JL, gl);
   return b;
 }
 
@@ -262,8 +233,8 @@ struct OutBuf {
 template <int LOG2G>
 constexpr uint32_t kOutLds = kFixLut<LOG2G, MainKeys> + 256u;  // after the fix-up LUT
 
-template <int LOG2G, int V, bool VERIFY>
-__device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const ColV<V>& A,
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
                                             int base, const MainKeys& kk, OutBuf ob);
 
@@ -284,14 +255,13 @@ __device__ __forceinline__ void body_prio_lo() {
 }
 
 // Fold, combine, check and emit one packet whose first batch is in `b`.
-template <int LOG2G, int V, bool VERIFY>
-__device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p,
-                                              Batch<kBodyU<V>, V>& b, int gl, int base,
-                                              const MainKeys& kk, OutBuf ob = {0, 0}) {
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, Batch<kUnroll>& b,
+                                              int gl, int base, const MainKeys& kk,
+                                              OutBuf ob = {0, 0}) {
   constexpr int G = 1 << LOG2G;
-  constexpr int CPL = 4 * V;
-  constexpr int DPI = G * CPL;
-  constexpr int U = kBodyU<V>;
+  constexpr int DPI = 4 * G;
+  constexpr int U = kUnroll;
   constexpr uint32_t kLut = kFixLut<LOG2G, MainKeys>;
   // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
   // U (the first block holds the remainder), then the last one (J-1), which
@@ -302,73 +272,61 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p,
   const int first = nbody == 0 ? 0 : ((nbody - 1) % U) + 1;
   const int nblk = (nbody + U - 1) / U;
 
-  ColV<V> A;
-#pragma unroll
-  for (int t = 0; t < CPL; ++t) A.P[t] = A.T[t] = 0;
+  Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < jhh; ++j) {
-    u32x4 w[V];
-    if (j < 2) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) w[v] = (j == 0) ? b.wh0[v] : b.wh1[v];
-    } else {
-      load_chunk<G, V>(w, p, j, gl);
-    }
-    const int kb = DPI * j + CPL * gl - p.S;
-#pragma unroll
-    for (int v = 0; v < V; ++v) fix_chunk5(w[v], kb + 4 * v, kLut, h0, h2);
-    foldV<V>(A, w, kk);
+    u32x4 w = (j == 0) ? b.wh0 : (j == 1) ? b.wh1 : load_chunk<G>(p, j, gl);
+    fix_chunk5(w, DPI * j + 4 * gl - p.S, kLut, h0, h2);
+    fold(A, w, kk);
   }
   // body blocks, ping-pong between b.cur and nxt (no register copies)
   int j0 = jhh, bs = first;
-  u32x4 nxt[U][V];
+  u32x4 nxt[U];
   for (int bk = 0; bk < nblk; bk += 2) {
     int jn = j0 + bs;
     if (bk + 1 < nblk) {
       body_prio_hi();
 #pragma unroll
-      for (int u = 0; u < U; ++u) load_body<G, V>(nxt[u], p, jn + u, gl);
+      for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
       body_prio_lo();
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (u < bs) foldV<V>(A, b.cur[u], kk);
+      if (u < bs) fold(A, b.cur[u], kk);
     if (bk + 1 >= nblk) break;
     j0 = jn;
     jn = j0 + U;
     if (bk + 2 < nblk) {
       body_prio_hi();
 #pragma unroll
-      for (int u = 0; u < U; ++u) load_body<G, V>(b.cur[u], p, jn + u, gl);
+      for (int u = 0; u < U; ++u) b.cur[u] = load_body<G>(p, jn + u, gl);
       body_prio_lo();
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) foldV<V>(A, nxt[u], kk);
+    for (int u = 0; u < U; ++u) fold(A, nxt[u], kk);
     j0 = jn;
     bs = U;
   }
   {
-    const int kb = DPI * JL + CPL * gl - p.S;
-    if (JL < p.jh) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) fix_chunk5(b.wl[v], kb + 4 * v, kLut, h0, h2);
-    }
-    fold_lastV<V>(A, b.wl, kb, p.n, kk);
+    u32x4 w = b.wl;
+    const int kb = DPI * JL + 4 * gl - p.S;
+    if (JL < p.jh) fix_chunk5(w, kb, kLut, h0, h2);
+    fold_last(A, w, kb, p.n, kk);
   }
-  emit_packet<LOG2G, V, VERIFY>(a, p, A, h0, h2, b.trailer, gl, base, kk, ob);
+  emit_packet<LOG2G, VERIFY>(a, p, A, h0, h2, b.trailer, gl, base, kk, ob);
 }
 
 // Packet done: fold the group's columns, check the header, emit.
-template <int LOG2G, int V, bool VERIFY>
-__device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const ColV<V>& A,
+template <int LOG2G, bool VERIFY>
+__device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
                                             int base, const MainKeys& kk, OutBuf ob) {
   constexpr int G = 1 << LOG2G;
-  constexpr int LC = kLog2Cpl<V>;
-  constexpr int DPI = G << LC;
-  uint32_t B = combineV<LOG2G, V, MainKeys>(A, p.r, gl, base);
-  uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> LC), 64);
-  uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> LC), 64);
+  constexpr int DPI = 4 * G;
+  uint32_t B = combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                        A.P[3] ^ A.T[3], p.r, gl, base);
+  uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
+  uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
   if (p.unal) {  // (per group) frame at an unaligned start: header bytes read directly
     d0 = ldg32_bytes(p.fp);
     d2 = ldg32_bytes(p.fp + 8);
@@ -388,8 +346,8 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
   }
   const bool good = (st & kPktFatal) == 0;
   if (good && (ihl != 5 || p.unal))
-    B = slow_packet<LOG2G, V>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl,
-                              gl, base, kk);
+    B = slow_packet<LOG2G>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl, gl,
+                           base, kk);
   const uint32_t icrc = good ? ~B : 0u;
   if (p.live && gl == 0) {
     if constexpr (VERIFY) {
@@ -411,17 +369,16 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
 }
 
 // Fixed-size frames at frames + i * stride.
-template <int LOG2G, int LV, bool VERIFY>
+template <int LOG2G, bool VERIFY>
 __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
-  constexpr int V = 1 << LV;
   constexpr int PPW = 64 / G;  // packets per wave step
   const int tid = threadIdx.x;
 #ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   const uint64_t c_start = __builtin_amdgcn_s_memtime();  // shader clock: the ratio is the GFX clock
 #endif
-  stage_tables<LOG2G, kIcrcThreads, MainKeys, LV>(a.tables, tid);
+  stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 
   const int lane = tid & 63;
@@ -435,7 +392,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
   const uint32_t set_begin = blockIdx.x * per_block;
   const uint32_t set_end = min(nsets, set_begin + per_block);
-  constexpr int DPI = 4 * G * V;
+  constexpr int DPI = 4 * G;
   auto make = [&](uint32_t set) {
     const uint32_t pkt = set * PPW + grp;
     const bool live = set < set_end && pkt < a.n;
@@ -453,8 +410,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   // measured: no gain at 4 KiB or 108-B frames, and register spills)
   for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kIcrcWaves) {
     const Pkt p = make(set);
-    Batch<kBodyU<V>, V> b = issue_packet<LOG2G, V, VERIFY>(p, gl);
-    finish_packet<LOG2G, V, VERIFY>(a, p, b, gl, grp * G, kk, ob);
+    Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+    finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk, ob);
   }
   if (a.icrc_out) {  // (uniform)
     __syncthreads();
@@ -492,12 +449,11 @@ struct RaggedLds {
   static constexpr uint32_t kBytes = kRlen + 2 * kWindow;
 };
 
-template <int LOG2G, int LV, bool VERIFY>
+template <int LOG2G, bool VERIFY>
 __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
-  constexpr int V = 1 << LV;
   constexpr int PPW = 64 / G;
-  constexpr int DPI = 4 * G * V;
+  constexpr int DPI = 4 * G;
   using LD = RaggedLds<LOG2G>;
   constexpr int W = LD::kWindow;
   constexpr int NB = LD::kBuckets;
@@ -506,7 +462,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 #ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  stage_tables<LOG2G, kIcrcThreads, MainKeys, LV>(a.tables, tid);
+  stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
 
   const int lane = tid & 63;
   const int gl = lane & (G - 1);
@@ -605,8 +561,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
       if (f + bk >= nsets) break;
       const int set = from_back ? nsets - 1 - bk : f;
       const Pkt p = make(set);
-      Batch<kBodyU<V>, V> b = issue_packet<LOG2G, V, VERIFY>(p, gl);
-      finish_packet<LOG2G, V, VERIFY>(a, p, b, gl, grp * G, kk);
+      Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk);
     }
     __syncthreads();
   }
@@ -842,30 +798,21 @@ __global__ void __launch_bounds__(1024) stream_read_kernel(const u32x4* __restri
 
 typedef void (*kernel_fn)(IcrcArgs);
 
-template <int LOG2G, int LV>
+template <int LOG2G>
 kernel_fn pick(bool ragged, bool verify) {
-  if (ragged)
-    return verify ? icrc_ragged_kernel<LOG2G, LV, true> : icrc_ragged_kernel<LOG2G, LV, false>;
-  return verify ? icrc_strided_kernel<LOG2G, LV, true> : icrc_strided_kernel<LOG2G, LV, false>;
+  if (ragged) return verify ? icrc_ragged_kernel<LOG2G, true> : icrc_ragged_kernel<LOG2G, false>;
+  return verify ? icrc_strided_kernel<LOG2G, true> : icrc_strided_kernel<LOG2G, false>;
 }
 
-// Instantiated (lanes per packet G = 2^log2g, chunks per lane V = 2^lv):
-// V = 1 for every G; V = 2 for G = 2, 4, 8; V = 4 for G = 1, 2, 4.
-kernel_fn select_kernel(int log2g, int lv, bool ragged, bool verify) {
-  switch (lv * 8 + log2g) {
-    case 0: return pick<0, 0>(ragged, verify);
-    case 1: return pick<1, 0>(ragged, verify);
-    case 2: return pick<2, 0>(ragged, verify);
-    case 3: return pick<3, 0>(ragged, verify);
-    case 4: return pick<4, 0>(ragged, verify);
-    case 5: return pick<5, 0>(ragged, verify);
-    case 6: return pick<6, 0>(ragged, verify);
-    case 9: return pick<1, 1>(ragged, verify);
-    case 10: return pick<2, 1>(ragged, verify);
-    case 11: return pick<3, 1>(ragged, verify);
-    case 16: return pick<0, 2>(ragged, verify);
-    case 17: return pick<1, 2>(ragged, verify);
-    case 18: return pick<2, 2>(ragged, verify);
+kernel_fn select_kernel(int log2g, bool ragged, bool verify) {
+  switch (log2g) {
+    case 0: return pick<0>(ragged, verify);
+    case 1: return pick<1>(ragged, verify);
+    case 2: return pick<2>(ragged, verify);
+    case 3: return pick<3>(ragged, verify);
+    case 4: return pick<4>(ragged, verify);
+    case 5: return pick<5>(ragged, verify);
+    case 6: return pick<6>(ragged, verify);
     default: return nullptr;
   }
 }
@@ -908,17 +855,14 @@ void build_table_image(uint32_t* out) {
 }
 
 hipError_t prepare_kernels() {
-  for (int lv = 0; lv <= 2; ++lv)
-    for (int l = 0; l <= kMaxLog2G; ++l)
-      for (int r = 0; r < 2; ++r)
-        for (int v = 0; v < 2; ++v) {
-          kernel_fn k = select_kernel(l, lv, r, v);
-          if (!k) continue;
-          hipError_t e = hipFuncSetAttribute((const void*)k,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds_bytes(l, r));
-          if (e != hipSuccess) return e;
-        }
+  for (int l = 0; l <= kMaxLog2G; ++l)
+    for (int r = 0; r < 2; ++r)
+      for (int v = 0; v < 2; ++v) {
+        hipError_t e = hipFuncSetAttribute((const void*)select_kernel(l, r, v),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_bytes(l, r));
+        if (e != hipSuccess) return e;
+      }
   for (int c : {4, 8})
     for (int v = 0; v < 2; ++v)
       for (int o = 0; o < 4; ++o) {
@@ -929,12 +873,10 @@ hipError_t prepare_kernels() {
   return prepare_segment_kernels();
 }
 
-bool has_chunks(int log2g, int lv) { return select_kernel(log2g, lv, false, false) != nullptr; }
-
-hipError_t launch_icrc(const IcrcArgs& a, int log2g, int lv, bool ragged, bool verify, int num_cus,
+hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
                        hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
-  kernel_fn k = select_kernel(log2g, lv, ragged, verify);
+  kernel_fn k = select_kernel(log2g, ragged, verify);
   if (!k) return hipErrorInvalidValue;
   const uint32_t ppw = 64u >> log2g;
   const uint64_t nsets = (a.n + ppw - 1) / ppw;
