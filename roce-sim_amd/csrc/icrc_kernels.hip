@@ -132,9 +132,17 @@ __device__ __forceinline__ u32x4 load_chunk_bytes(const Pkt& p, int j, int gl) {
 }
 
 // Body iterations (jh <= j < J-1) lie wholly inside the frame: no predicate.
+// A block's U loads go out from one 64-bit address per block (the lane's
+// chunk of iteration j) with the iteration steps as immediate offsets
+// (16 G u < 4 KiB), instead of a 64-bit address build per load.
 template <int G>
-__device__ __forceinline__ u32x4 load_body(const Pkt& p, int j, int gl) {
-  return ldg128(p.ab + 16 * (G * j + gl));
+__device__ __forceinline__ const uint8_t* body_addr(const Pkt& p, int j, int gl) {
+  return p.ab + (uint32_t)(16 * (G * j + gl));  // (frame-relative offsets stay below 2^17)
+}
+template <int G, int U>
+__device__ __forceinline__ void load_block(u32x4 (&w)[U], const uint8_t* q) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) w[u] = ldg128(q + 16 * G * u);
 }
 
 
@@ -217,9 +225,11 @@ __device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
   if (VERIFY && !p.dead && gl == 0) b.trailer = ldg32(p.fp + p.L - 4);
   b.wh0 = jhh > 0 ? load_chunk<G>(p, 0, gl) : u32x4{0, 0, 0, 0};
   b.wh1 = jhh > 1 ? load_chunk<G>(p, 1, gl) : u32x4{0, 0, 0, 0};
+  {
+    const uint8_t* q = body_addr<G>(p, jhh, gl);
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    b.cur[u] = u < first ? load_body<G>(p, jhh + u, gl) : u32x4{0, 0, 0, 0};
+    for (int u = 0; u < U; ++u) b.cur[u] = u < first ? ldg128(q + 16 * G * u) : u32x4{0, 0, 0, 0};
+  }
   b.wl = load_chunk<G>(p, JL, gl);
   return b;
 }
@@ -286,8 +296,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     int jn = j0 + bs;
     if (bk + 1 < nblk) {
       body_prio_hi();
-#pragma unroll
-      for (int u = 0; u < U; ++u) nxt[u] = load_body<G>(p, jn + u, gl);
+      load_block<G, U>(nxt, body_addr<G>(p, jn, gl));
       body_prio_lo();
     }
 #pragma unroll
@@ -298,8 +307,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     jn = j0 + U;
     if (bk + 2 < nblk) {
       body_prio_hi();
-#pragma unroll
-      for (int u = 0; u < U; ++u) b.cur[u] = load_body<G>(p, jn + u, gl);
+      load_block<G, U>(b.cur, body_addr<G>(p, jn, gl));
       body_prio_lo();
     }
 #pragma unroll
