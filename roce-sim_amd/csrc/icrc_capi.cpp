@@ -25,6 +25,9 @@ struct ricrc_ctx {
   int lanes = 0;  // 0 = automatic
   hipStream_t stream = nullptr;
   uint32_t* d_tables = nullptr;
+  // tail-claim counters of the strided kernel (kClaimSlots x kMaxClaimBlocks)
+  unsigned long long* d_claims = nullptr;
+  uint32_t claim_epoch = 0;
   // scratch for the host-buffer entry points
   uint8_t* d_frames = nullptr;
   size_t frames_cap = 0;
@@ -164,10 +167,15 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   a.ok_out = ok;
   a.tables = c->d_tables;
   HIP_TRY(hipSetDevice(c->device));
-  if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0)
+  if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0) {
     HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
-  else
+  } else {
+    if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) {
+      a.claims = c->d_claims;
+      a.epoch = ++c->claim_epoch;  // (slot epoch % kClaimSlots of the counters)
+    }
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
+  }
   return RICRC_OK;
 }
 
@@ -369,6 +377,9 @@ int ricrc_ctx_create(int device, ricrc_ctx** out) {
   ricrc::build_table_image(img.data());
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->d_tables, img.size() * sizeof(uint32_t));
+  const size_t claim_bytes = sizeof(unsigned long long) * ricrc::kClaimSlots * ricrc::kMaxClaimBlocks;
+  if (e == hipSuccess) e = hipMalloc(&c->d_claims, claim_bytes);
+  if (e == hipSuccess) e = hipMemset(c->d_claims, 0, claim_bytes);
   if (e == hipSuccess)
     e = hipMemcpy(c->d_tables, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -384,6 +395,7 @@ void ricrc_ctx_destroy(ricrc_ctx* c) {
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   (void)hipFree(c->d_tables);
+  (void)hipFree(c->d_claims);
   (void)hipFree(c->d_frames);
   (void)hipFree(c->d_offs);
   (void)hipFree(c->d_lens);

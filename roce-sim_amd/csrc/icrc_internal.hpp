@@ -25,7 +25,16 @@ struct IcrcArgs {
   uint8_t* status_out;  // nullable
   uint8_t* ok_out;      // verify mode
   const uint32_t* tables;
+  // strided lane-group kernel: per-workgroup claim counters for the tail of
+  // its range (epoch << 32 | next), nullable = static ranges only
+  unsigned long long* claims;
+  uint32_t epoch;
 };
+
+// Claim counters: kClaimSlots launches of one context may be in flight at
+// once (slot = epoch % kClaimSlots), each with one counter per workgroup.
+constexpr int kClaimSlots = 64;
+constexpr int kMaxClaimBlocks = 1024;
 
 // Builds the table image on the host (kTableWords words).
 void build_table_image(uint32_t* out);

@@ -376,6 +376,18 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
   }
 }
 
+// Tail stealing (strided kernel): the last 1/kTailDiv of a workgroup's sets
+// are claimed dynamically; a finished wave tries up to kMaxVictims other
+// workgroups' tails.
+#ifndef RICRC_TAIL_DIV
+#define RICRC_TAIL_DIV 4
+#endif
+constexpr uint32_t kTailDiv = RICRC_TAIL_DIV;
+#ifndef RICRC_MAX_VICTIMS
+#define RICRC_MAX_VICTIMS 4
+#endif
+constexpr uint32_t kMaxVictims = RICRC_MAX_VICTIMS;
+
 // Fixed-size frames at frames + i * stride.
 template <int LOG2G, bool VERIFY>
 __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs a) {
@@ -398,12 +410,24 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   // grid-interleaved sets); its 16 waves take consecutive sets of that range.
   const uint32_t nsets = (a.n + PPW - 1) / PPW;
   const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
-  const uint32_t set_begin = blockIdx.x * per_block;
-  const uint32_t set_end = min(nsets, set_begin + per_block);
+  // A workgroup's range [begin, end) of sets; its last 1/kTailDiv ("tail")
+  // is claimed set by set through a counter that other workgroups may also
+  // claim from once their own range is done (see below).
+  auto range = [&](uint32_t blk, uint32_t& b, uint32_t& e, uint32_t& split) {
+    b = blk * per_block;
+    e = min(nsets, b + per_block);
+    const uint32_t len = b < e ? e - b : 0u;
+    split = e - (a.claims ? len / kTailDiv : 0u);
+  };
+  uint32_t set_begin, set_end, set_split;
+  range(blockIdx.x, set_begin, set_end, set_split);
+  unsigned long long* claims =
+      a.claims ? a.claims + (size_t)(a.epoch % kClaimSlots) * kMaxClaimBlocks : nullptr;
+  if (claims && tid == 0) atomicExch(&claims[blockIdx.x], (unsigned long long)a.epoch << 32);
   constexpr int DPI = 4 * G;
   auto make = [&](uint32_t set) {
     const uint32_t pkt = set * PPW + grp;
-    const bool live = set < set_end && pkt < a.n;
+    const bool live = set < nsets && pkt < a.n;
     return describe<DPI>(a.frames, pkt, live, live ? (uint64_t)pkt * a.stride : 0,
                          live ? a.len : 0);
   };
@@ -411,15 +435,51 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   // coalesced run at the end: 4-byte words written while the frames stream in
   // cost 2.5 % at cfg2 (measured with the stores ablated), HBM writes mixed
   // into the read stream being expensive (small-frame kernel).
+  // Only the statically owned sets use the buffer (tail sets may be claimed
+  // by another workgroup, which writes their words straight to icrc_out).
   const uint32_t p0 = set_begin * PPW;
-  const uint32_t p1 = set_begin < set_end ? min(a.n, set_end * PPW) : p0;
+  const uint32_t p1 = set_begin < set_split ? min(a.n, set_split * PPW) : p0;
   const OutBuf ob = {p0, min(p1 - p0, (163840u - kOutLds<LOG2G>) / 4u)};
   // (issuing the next set's first batch before finishing this one was
   // measured: no gain at 4 KiB or 108-B frames, and register spills)
-  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kIcrcWaves) {
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_split;
+       set += (uint32_t)kIcrcWaves) {
     const Pkt p = make(set);
     Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
     finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk, ob);
+  }
+  // Tail: the workgroups on some XCDs stream measurably slower than others
+  // (cfg2: odd XCDs end ~3 % later), so with static ranges the launch waits
+  // for the slowest.  A wave that is done claims single sets from its own
+  // tail (one returning atomic per set on its workgroup's counter, issued
+  // one set ahead so its latency hides behind the current set), then from
+  // the tails of workgroups blk + 1, blk + 3, ... (the other XCD parity
+  // first), up to kMaxVictims of them.  A counter still holding an older
+  // epoch (its owner has not started yet) counts as empty.
+  if (claims) {
+    uint32_t victim = blockIdx.x, tries = 0;
+    auto claim = [&](uint32_t v) -> uint32_t {  // set index, or ~0u if v's tail is empty
+      unsigned long long old = 0;
+      if (lane == 0) old = atomicAdd(&claims[v], 1ull);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)old);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(old >> 32));
+      uint32_t vb, ve, vs;
+      range(v, vb, ve, vs);
+      return (hi == a.epoch && lo < ve - vs) ? vs + lo : ~0u;
+    };
+    uint32_t cur = claim(victim);
+    for (;;) {
+      if (cur == ~0u) {
+        if (++tries > kMaxVictims) break;
+        victim = (blockIdx.x + 2 * tries - 1) % gridDim.x;
+        cur = claim(victim);
+        continue;
+      }
+      const Pkt p = make(cur);
+      Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+      cur = claim(victim);  // the next set, while this one streams in
+      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk, OutBuf{0, 0});
+    }
   }
   if (a.icrc_out) {  // (uniform)
     __syncthreads();

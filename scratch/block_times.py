@@ -25,7 +25,11 @@ def report(tag, st, nblk):
                       "end_min_us": float(end.min()), "end_med_us": float(np.median(end)),
                       "end_max_us": float(end.max()), "dur_min_us": float(dur.min()),
                       "dur_max_us": float(dur.max()),
-                      "tail_frac": float((end.max() - np.median(end)) / end.max())}), flush=True)
+                      "tail_frac": float((end.max() - np.median(end)) / end.max()),
+                      # workgroup b runs on XCD b % 8 (round-robin dispatch)
+                      "xcd_end_med_us": [round(float(np.median(end[x::8])), 1) for x in range(8)],
+                      "xcd_start_med_us": [round(float(np.median(start[x::8])), 1)
+                                           for x in range(8)]}), flush=True)
 
 
 def main():

@@ -359,6 +359,30 @@ def test_device_resident_torch(engine):
     assert okc[7] == 0 and okc.sum() == n - 1
 
 
+def test_strided_tail_claims_concurrent_streams(engine):
+    """The strided kernel's workgroups claim the tails of their ranges (and of
+    other workgroups' ranges) through per-context counters: launches of ONE
+    context in flight on several streams at once, and many back-to-back
+    launches (counter slots reused every 64 epochs), stay bit-exact; so do
+    batch sizes whose ranges are shorter than a tail (few sets per block)."""
+    torch = pytest.importorskip("torch")
+    sizes = [1 << 16, 3 * 257 + 5, 8 * 256 * 4 + 1, 77]
+    data = []
+    for i, n in enumerate(sizes):
+        buf, stride, flen = synth.uniform_frames(n, 4096, seed=40 + i)
+        want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+        data.append((torch.from_numpy(buf).cuda(), stride, flen, n, want))
+    streams = [torch.cuda.Stream() for _ in sizes]
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _, _, _, n, _ in data]
+    torch.cuda.synchronize()
+    for rep in range(40):  # 160 launches: every claim slot is reused
+        for (d, stride, flen, n, _), out, st in zip(data, outs, streams):
+            engine.compute_strided_dev(d, stride, flen, n, out, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for (_, _, _, _, want), out in zip(data, outs):
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
 def test_multi_context_round_robin(engine):
     from roce_icrc import IcrcEngine, compute_batch_multi
     n = 3001
