@@ -668,10 +668,17 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 // LDS: [0, 64 KiB) Mul(128) in the Keys16 layout (icrc_device.hpp: 16
 // conflict-free copies, one v_perm_b32 per address), [64, 68 KiB) Mul(-32),
 // then one staging slot of 64 x stride bytes per wave.
-constexpr int kSmallMaxWaves = 12;
+#ifndef RICRC_SMALL_WAVES
+#define RICRC_SMALL_WAVES 8
+#endif
+constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
 constexpr uint32_t kSmallComb = Keys16::kComb;
 constexpr uint32_t kSmallStage = kSmallComb + 4096;
 constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + 3) / 4;  // ns <= 8
+#ifndef RICRC_SMALL_OUTBUF
+#define RICRC_SMALL_OUTBUF 64
+#endif
+constexpr int kSmallOutRounds = RICRC_SMALL_OUTBUF;  // output ring depth in rounds (0 = off)
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
@@ -716,7 +723,17 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     }
     return st;
   };
-  auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer) {
+  // Output ring (compute mode with icrc_out): the ICRC words of kOutRounds
+  // rounds of nw batches (one batch per wave) collect in LDS after the
+  // staging slots, and the workgroup writes them out together as one
+  // contiguous run of 16-byte stores between two barriers, instead of each
+  // wave storing 256 B per batch into the read stream.
+  constexpr bool kRing = kSmallOutRounds > 0 && (OUTS & 1) != 0 && !VERIFY;
+  const uint32_t ring = kSmallStage + nw * 64u * S;
+  const uint32_t rounds_cap = kRing ? min((uint32_t)kSmallOutRounds, (163840u - ring) / (nw * 256u)) : 0u;
+  uint32_t ring_base = 0;  // first packet of the ring's current window
+  auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer,
+                  bool to_ring = false) {
     const bool good = (st & kPktFatal) == 0;
     const uint32_t icrc = good ? ~R : 0u;
     if (live) {
@@ -728,7 +745,12 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
 #ifdef RICRC_SMALL_STORE_RING  // diagnostic build only: outputs wrap in a ring of that many dwords
       if constexpr ((OUTS & 1) != 0) a.icrc_out[pkt & (RICRC_SMALL_STORE_RING - 1u)] = icrc;
 #else
-      if constexpr ((OUTS & 1) != 0) a.icrc_out[pkt] = icrc;
+      if constexpr ((OUTS & 1) != 0) {
+        if (kRing && to_ring)
+          lds_wr(ring + 4u * (pkt - ring_base), icrc);
+        else
+          a.icrc_out[pkt] = icrc;
+      }
 #endif
       if constexpr ((OUTS & 2) != 0) a.status_out[pkt] = (uint8_t)st;
     }
@@ -762,7 +784,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
 #pragma unroll
     for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
   };
-  auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext) {
+  auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext, bool live = true) {
 #ifdef RICRC_SMALL_ABLATE_STAGE  // diagnostic build only: loads and output stores, no LDS, no fold
     {
       u32x4 acc = Rg[0];
@@ -808,7 +830,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     } else {
       R = fold4_masked(ihl, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
     }
-    emit(b * 64u + (uint32_t)lane, true, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u);
+    emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing);
     __asm__ __volatile__("" ::: "memory");
   };
 
@@ -816,7 +838,41 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   // loads are issued two batches ahead (buffers X, Y), right after the batch
   // that used the buffer is staged (a third buffer measured no faster)
   const uint32_t bs_end = min(b1, last);
-  if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
+  if (kRing && rounds_cap > 0 && b0 < bs_end) {  // (uniform)
+    // rounds: round r is batch b0 + r nw + wave of every wave (waves past
+    // bs_end recompute a clamped batch and emit nothing); every rounds_cap
+    // rounds the ring goes out.  LDS-only waits at the barriers: the
+    // prefetched loads stay in flight across them.
+    const uint32_t nrounds = (bs_end - b0 + nw - 1) / nw;
+    u32x4 X[C], Y[C];
+    load(b0 + (uint32_t)wave, X);
+    load(b0 + (uint32_t)wave + nw, Y);
+    ring_base = b0 * 64u;
+    uint32_t in_ring = 0;
+    auto flush = [&]() {
+      const uint32_t words = min(in_ring * nw, bs_end - ring_base / 64u) * 64u;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring words are written
+      __builtin_amdgcn_s_barrier();
+      u32x4* dst = (u32x4*)(a.icrc_out + ring_base);
+      for (uint32_t i = (uint32_t)tid; i < words / 4u; i += blockDim.x)
+        dst[i] = *(const lds_u32x4*)(uintptr_t)(ring + 16u * i);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // the ring is read before anyone writes it again
+      __builtin_amdgcn_s_barrier();
+      ring_base += in_ring * nw * 64u;
+      in_ring = 0;
+    };
+    for (uint32_t r = 0; r < nrounds; r += 2) {
+      uint32_t b = b0 + r * nw + (uint32_t)wave;
+      stage_and_fold(b, X, b + 2 * nw, b < bs_end);
+      if (++in_ring == rounds_cap) flush();
+      if (r + 1 < nrounds) {
+        b += nw;
+        stage_and_fold(b, Y, b + 2 * nw, b < bs_end);
+        if (++in_ring == rounds_cap) flush();
+      }
+    }
+    if (in_ring) flush();
+  } else if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
     const uint32_t first = b0 + (uint32_t)wave;
     const int cnt = first < bs_end ? (int)((bs_end - first + nw - 1) / nw) : 0;
     u32x4 X[C], Y[C];
@@ -963,7 +1019,7 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   kernel_fn k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;
   const uint32_t nw = min((uint32_t)kSmallMaxWaves, (163840u - kSmallStage) / slot);
-  const size_t lds = kSmallStage + (size_t)nw * slot;
+  const size_t lds = 163840;  // staging slots, then the output ring in what is left
   const uint64_t nb = (a.n + 63) / 64;
   uint64_t blocks = (nb + nw - 1) / nw;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
