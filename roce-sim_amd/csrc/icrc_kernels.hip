@@ -357,7 +357,11 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
     B = slow_packet<LOG2G>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl, gl,
                            base, kk);
   const uint32_t icrc = good ? ~B : 0u;
+#ifdef RICRC_ABLATE_OUT  // diagnostic build only: per-packet output stores removed (kept live)
+  if (p.live && gl == 0 && icrc == 0x9E3779B9u) {
+#else
   if (p.live && gl == 0) {
+#endif
     if constexpr (VERIFY) {
       const bool ok = good && trailer == icrc;
       if (good && !ok) st |= kPktIcrcMismatch;
