@@ -365,17 +365,17 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
     if constexpr (VERIFY) {
       const bool ok = good && trailer == icrc;
       if (good && !ok) st |= kPktIcrcMismatch;
-      a.ok_out[p.pkt] = ok ? 1 : 0;
+      stg8<kPktStorePol>(a.ok_out + p.pkt, ok ? 1u : 0u);
     }
     if (a.icrc_out) {
       const uint32_t k = p.pkt - ob.p0;
       if (k < ob.cap)
         lds_wr(kOutLds<LOG2G> + 4u * k, icrc);
       else
-        a.icrc_out[p.pkt] = icrc;
+        stg32<kPktStorePol>(a.icrc_out + p.pkt, icrc);
     }
 #ifndef RICRC_BLOCK_TIMES
-    if (a.status_out) a.status_out[p.pkt] = (uint8_t)st;
+    if (a.status_out) stg8<kPktStorePol>(a.status_out + p.pkt, st);
 #endif
   }
 }
@@ -391,6 +391,14 @@ constexpr uint32_t kTailDiv = RICRC_TAIL_DIV;
 #define RICRC_MAX_VICTIMS 4
 #endif
 constexpr uint32_t kMaxVictims = RICRC_MAX_VICTIMS;
+
+// Cache policy of the block's output run (out_store128): default.  The run
+// goes out at the end of the block, when the rest of the chip still streams;
+// sc1 measured 0.5 % slower on cfg2 (3 A/B rounds).
+#ifndef RICRC_STRIDED_OUT_POL
+#define RICRC_STRIDED_OUT_POL 0
+#endif
+constexpr int kStridedOutPol = RICRC_STRIDED_OUT_POL;
 
 // Fixed-size frames at frames + i * stride.
 template <int LOG2G, bool VERIFY>
@@ -487,8 +495,12 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   }
   if (a.icrc_out) {  // (uniform)
     __syncthreads();
-    for (uint32_t i = (uint32_t)tid; i < ob.cap; i += kIcrcThreads)
-      a.icrc_out[p0 + i] = lds_rd(kOutLds<LOG2G> + 4u * i);
+    const auto dst = out_rsrc(a.icrc_out + p0, 4u * ob.cap);
+    for (uint32_t i = (uint32_t)tid; i < ob.cap / 4u; i += kIcrcThreads)
+      out_store128<kStridedOutPol>(*(const lds_u32x4*)(uintptr_t)(kOutLds<LOG2G> + 16u * i), dst,
+                                   16u * i);
+    for (uint32_t i = (ob.cap & ~3u) + (uint32_t)tid; i < ob.cap; i += kIcrcThreads)
+      out_store32<kStridedOutPol>(lds_rd(kOutLds<LOG2G> + 4u * i), dst, 4u * i);
   }
 #ifdef RICRC_BLOCK_TIMES
   __syncthreads();
@@ -683,6 +695,19 @@ constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + 3) / 4;  // ns <= 8
 #define RICRC_SMALL_OUTBUF 64
 #endif
 constexpr int kSmallOutRounds = RICRC_SMALL_OUTBUF;  // output ring depth in rounds (0 = off)
+// Cache policy of the ring's flushes (out_store128).  The words written into
+// the saturating read stream cost several times their own transfer time;
+// scope-sc1 stores cut that: cfg5 4625 -> 4865 GiB/s (3 A/B rounds; nt the
+// same, 4870).  Microbenchmark (scratch/rw_mix.hip, read pattern without the
+// CRC): read only 0.266 ms, + words flushed every 16 rounds plain 0.325, nt
+// 0.314, sc1 0.307; every 30 rounds with sc1 0.293 (larger bursts are
+// cheaper, but the ring cannot grow beside 8 staging slots); a 9th "writer"
+// wave draining the ring, with or without bursts aligned to a global clock,
+// 0.320-0.344.
+#ifndef RICRC_SMALL_OUT_POL
+#define RICRC_SMALL_OUT_POL 16
+#endif
+constexpr int kSmallOutPol = RICRC_SMALL_OUT_POL;
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
@@ -857,9 +882,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       const uint32_t words = min(in_ring * nw, bs_end - ring_base / 64u) * 64u;
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring words are written
       __builtin_amdgcn_s_barrier();
-      u32x4* dst = (u32x4*)(a.icrc_out + ring_base);
+      const auto dst = out_rsrc(a.icrc_out + ring_base, 4u * words);
       for (uint32_t i = (uint32_t)tid; i < words / 4u; i += blockDim.x)
-        dst[i] = *(const lds_u32x4*)(uintptr_t)(ring + 16u * i);
+        out_store128<kSmallOutPol>(*(const lds_u32x4*)(uintptr_t)(ring + 16u * i), dst, 16u * i);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // the ring is read before anyone writes it again
       __builtin_amdgcn_s_barrier();
       ring_base += in_ring * nw * 64u;

@@ -57,6 +57,11 @@ __device__ __forceinline__ u32x4 ldmr(const uint8_t* p) {
 constexpr int kSegUnroll = RICRC_SEG_UNROLL;  // body iterations (16-byte MR loads per lane) in flight
 constexpr int kSegThreads = RICRC_SEG_THREADS;  // one workgroup per CU (the tables fill the LDS)
 constexpr int kSegWaves = kSegThreads / 64;
+// Cache policy of the frame stores (stg128 in icrc_device.hpp; 2 = nt).
+#ifndef RICRC_SEG_STORE_POL
+#define RICRC_SEG_STORE_POL 2
+#endif
+constexpr int kSegStorePol = RICRC_SEG_STORE_POL;
 constexpr uint32_t kRocePort = 4791;   // src/roce_enum.py ROCE_PORT
 constexpr uint32_t kAckValue = 31;     // CREDIT_CNT_INVALID, src/roce_enum.py:8
 constexpr uint32_t kPktSegBad = 0x20;  // RICRC_PKT_SEG_BAD
@@ -348,7 +353,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
       else if (j == Jw - 1)
         holdL = w;
       else
-        __builtin_nontemporal_store(w, (u32x4*)(s.dst + 4 * idx0));
+        stg128<kSegStorePol>(s.dst + 4 * idx0, w);
       if (j < J) {  // CRC: masked header dwords, seed, columns past the end skipped
         w.x = fix_dword(w.x, idx0 + 0, 6, 8);
         w.y = fix_dword(w.y, idx0 + 1, 6, 8);
@@ -368,7 +373,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
         uint8_t* d = s.dst + 4 * (DPI * j0 + 4 * gl);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          __builtin_nontemporal_store(v[u], (u32x4*)(d + 4 * DPI * u));
+          stg128<kSegStorePol>(d + 4 * DPI * u, v[u]);
           csum_add(acc, v[u]);
           fold(A, v[u], kk);
         }
@@ -459,8 +464,8 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
         h.z = t == 2 ? icrc : h.z;
         h.w = t == 3 ? icrc : h.w;
       }
-      if (4 * gl < s.T) __builtin_nontemporal_store(hold0, (u32x4*)(s.dst + 16 * gl));
-      if (jl > 0 && idxL < s.T) __builtin_nontemporal_store(holdL, (u32x4*)(s.dst + 4 * idxL));
+      if (4 * gl < s.T) stg128<kSegStorePol>(s.dst + 16 * gl, hold0);
+      if (jl > 0 && idxL < s.T) stg128<kSegStorePol>(s.dst + 4 * idxL, holdL);
     }
     if (pkt < a.npkts && gl == 0) {
       a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;
