@@ -206,8 +206,9 @@ struct Keys32 {
   template <int THREADS>
   __device__ static void stage(const uint32_t* m, int tid) {
 #pragma unroll
-    for (int r = 0; r < 8192 / THREADS; ++r) {
+    for (int r = 0; r < (8192 + THREADS - 1) / THREADS; ++r) {
       const int i = tid + r * THREADS;  // 8192 16-byte quads
+      if (8192 % THREADS != 0 && i >= 8192) break;
       const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
       lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), m[tab * 256 + e]);
     }

@@ -51,11 +51,23 @@ namespace {
 
 
 // Lane-group kernels: one workgroup per CU (the replicated tables fill the LDS).
+// Ragged: 16 waves (its short sorted sets are instruction-bound: 12 waves
+// measured 5 % slower on cfg3).  Strided: 12 waves.  With 16 waves x 8
+// 16-byte loads per lane in flight a CU holds 128 KiB of reads in flight,
+// past what HBM serves best: a pure read stream runs at 7.13 TB/s with
+// 64 KiB in flight per CU and 6.70 with 128 KiB (scratch/read_ceiling.hip);
+// cfg2 at 12 waves +2 % (6050 -> 6179 GiB/s, 3 A/B rounds; 10 waves +1.7 %,
+// 8 waves -1 %).
 #ifndef RICRC_THREADS
 #define RICRC_THREADS 1024
 #endif
-constexpr int kIcrcThreads = RICRC_THREADS;
+#ifndef RICRC_STRIDED_THREADS
+#define RICRC_STRIDED_THREADS 768
+#endif
+constexpr int kIcrcThreads = RICRC_THREADS;  // ragged kernel
 constexpr int kIcrcWaves = kIcrcThreads / 64;
+constexpr int kStridedThreads = RICRC_STRIDED_THREADS;
+constexpr int kStridedWaves = kStridedThreads / 64;
 
 constexpr uint32_t kPktBadLen = 0x01, kPktNotIpv4 = 0x02, kPktNotUdp = 0x04,
                    kPktLenMismatch = 0x08, kPktIcrcMismatch = 0x10,
@@ -402,7 +414,7 @@ constexpr int kStridedOutPol = RICRC_STRIDED_OUT_POL;
 
 // Fixed-size frames at frames + i * stride.
 template <int LOG2G, bool VERIFY>
-__global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs a) {
+__global__ void __launch_bounds__(kStridedThreads, 1) icrc_strided_kernel(IcrcArgs a) {
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;  // packets per wave step
   const int tid = threadIdx.x;
@@ -410,7 +422,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   const uint64_t c_start = __builtin_amdgcn_s_memtime();  // shader clock: the ratio is the GFX clock
 #endif
-  stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
+  stage_tables<LOG2G, kStridedThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 
   const int lane = tid & 63;
@@ -455,7 +467,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   // (issuing the next set's first batch before finishing this one was
   // measured: no gain at 4 KiB or 108-B frames, and register spills)
   for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_split;
-       set += (uint32_t)kIcrcWaves) {
+       set += (uint32_t)kStridedWaves) {
     const Pkt p = make(set);
     Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
     finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk, ob);
@@ -496,10 +508,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_strided_kernel(IcrcArgs 
   if (a.icrc_out) {  // (uniform)
     __syncthreads();
     const auto dst = out_rsrc(a.icrc_out + p0, 4u * ob.cap);
-    for (uint32_t i = (uint32_t)tid; i < ob.cap / 4u; i += kIcrcThreads)
+    for (uint32_t i = (uint32_t)tid; i < ob.cap / 4u; i += kStridedThreads)
       out_store128<kStridedOutPol>(*(const lds_u32x4*)(uintptr_t)(kOutLds<LOG2G> + 16u * i), dst,
                                    16u * i);
-    for (uint32_t i = (ob.cap & ~3u) + (uint32_t)tid; i < ob.cap; i += kIcrcThreads)
+    for (uint32_t i = (ob.cap & ~3u) + (uint32_t)tid; i < ob.cap; i += kStridedThreads)
       out_store32<kStridedOutPol>(lds_rd(kOutLds<LOG2G> + 4u * i), dst, 4u * i);
   }
 #ifdef RICRC_BLOCK_TIMES
@@ -927,24 +939,29 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   }
 }
 
-// STREAM-style read ceiling with the same geometry as the ICRC kernel: one
-// 1024-thread workgroup per CU sweeping a contiguous chunk, 16-B nt loads.
-__global__ void __launch_bounds__(1024) stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
-                                                           uint32_t* sink) {
+// STREAM-style read ceiling: one workgroup per CU sweeping a contiguous
+// chunk with 16-byte nt loads, 8 per lane, 8 waves (64 KiB in flight per CU).
+// Sweep over the cfg2 buffer (scratch/read_ceiling.hip): this shape 7.13 TB/s;
+// 16 waves x 8 loads (the round-1 ceiling kernel) 6.70; ping-pong buffers
+// 7.10 at 64 KiB in flight, 6.8-7.0 at 128 KiB; plain loads 5.95-6.18.
+constexpr int kStreamThreads = 512;
+__global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4* __restrict__ p,
+                                                                     uint64_t n16, uint32_t* sink) {
   constexpr int R = 8;
+  constexpr uint64_t T = kStreamThreads;
   const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * per;
   const uint64_t b1 = b0 + per < n16 ? b0 + per : n16;
   u32x4 acc = {0, 0, 0, 0};
   uint64_t i = b0 + threadIdx.x;
-  for (; i + (R - 1) * 1024 < b1; i += R * 1024) {
+  for (; i + (R - 1) * T < b1; i += R * T) {
     u32x4 v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load(p + i + r * 1024);
+    for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load(p + i + r * T);
 #pragma unroll
     for (int r = 0; r < R; ++r) acc ^= v[r];
   }
-  for (; i < b1; i += 1024) acc ^= p[i];
+  for (; i < b1; i += T) acc ^= p[i];
   const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
   if (x == 0x9E3779B9u) sink[0] = x;  // keeps the loads live; practically never stores
 }
@@ -1033,10 +1050,11 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   if (!k) return hipErrorInvalidValue;
   const uint32_t ppw = 64u >> log2g;
   const uint64_t nsets = (a.n + ppw - 1) / ppw;
-  uint64_t blocks = (nsets + kIcrcWaves - 1) / kIcrcWaves;
+  const int waves = ragged ? kIcrcWaves : kStridedWaves;
+  uint64_t blocks = (nsets + waves - 1) / waves;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kIcrcThreads), lds_bytes(log2g, ragged), stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * waves), lds_bytes(log2g, ragged), stream, a);
   return hipGetLastError();
 }
 
@@ -1060,7 +1078,7 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink
                               hipStream_t stream) {
   const uint64_t n16 = bytes / 16;
   if (n16 == 0) return hipSuccess;
-  hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)num_cus), dim3(1024), 0, stream,
+  hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)num_cus), dim3(kStreamThreads), 0, stream,
                      (const u32x4*)buf, n16, sink);
   return hipGetLastError();
 }

@@ -1,0 +1,134 @@
+// What is the HBM read ceiling of MI355X for a once-read stream?  Sweeps a
+// pure-read kernel over the cfg2 frame buffer size (4.34 GB): threads per
+// CU, 16-byte loads in flight per lane, wait-all vs ping-pong buffers, and
+// the wave access pattern (the workgroup's waves interleaved per instruction
+// vs one contiguous sub-range per wave).  One workgroup per CU, per-CU
+// contiguous range, nt loads unless noted.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+// wait-all: R loads, then consume (what bench.py's ceiling kernel does)
+template <int R, bool NT>
+__global__ void __launch_bounds__(1024) rd_waitall(const u32x4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(n16, b0 + per);
+  const uint32_t T = blockDim.x;
+  u32x4 acc = {0, 0, 0, 0};
+  uint64_t i = b0 + threadIdx.x;
+  for (; i + (uint64_t)(R - 1) * T < b1; i += (uint64_t)R * T) {
+    u32x4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = ld<NT>(p + i + r * T);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc ^= v[r];
+  }
+  for (; i < b1; i += T) acc ^= p[i];
+  const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// ping-pong: two register buffers of R loads, the next one in flight while
+// the current one is consumed.  WAVE_CONTIG: each wave sweeps its own
+// contiguous sub-range (64 lanes x 16 B = 1 KiB per instruction).
+template <int R, bool NT, bool WAVE_CONTIG>
+__global__ void __launch_bounds__(1024) rd_pingpong(const u32x4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(n16, b0 + per);
+  const uint32_t T = blockDim.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NWv = T >> 6;
+  uint64_t start, step, end;
+  if (WAVE_CONTIG) {
+    const uint64_t wper = ((b1 - b0) / NWv) & ~(uint64_t)63;
+    start = b0 + wave * wper + lane;
+    end = wave + 1 == NWv ? b1 : b0 + (wave + 1) * wper;
+    step = 64;
+  } else {
+    start = b0 + threadIdx.x;
+    end = b1;
+    step = T;
+  }
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 X[R], Y[R];
+  const uint64_t blk = (uint64_t)R * step;
+  uint64_t i = start;
+  auto load = [&](u32x4* V, uint64_t at) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) V[r] = ld<NT>(p + min(at + r * step, b1 - 1));
+  };
+  load(X, i);
+  load(Y, i + blk);
+  for (; i < end; i += 2 * blk) {  // (reads past the range clamp to its last chunk: cache hits)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc ^= X[r];
+    load(X, i + 2 * blk);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc ^= Y[r];
+    load(Y, i + 3 * blk);
+  }
+  const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// copy: R nt loads then R nt (or plain) stores per lane
+template <int R, bool NTS>
+__global__ void __launch_bounds__(1024) cp_waitall(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(n16, b0 + per);
+  const uint32_t T = blockDim.x;
+  uint64_t i = b0 + threadIdx.x;
+  for (; i + (uint64_t)(R - 1) * T < b1; i += (uint64_t)R * T) {
+    u32x4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load(src + i + r * T);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (NTS) __builtin_nontemporal_store(v[r], dst + i + r * T); else dst[i + r * T] = v[r];
+    }
+  }
+  for (; i < b1; i += T) dst[i] = src[i];
+}
+
+int main() {
+  const uint64_t bytes = 4341104640ull;  // cfg2: 2^20 x 4140 B
+  const uint64_t n16 = bytes / 16;
+  uint8_t* d; uint32_t* sink;
+  CK(hipMalloc(&d, bytes)); CK(hipMalloc(&sink, 64));
+  CK(hipMemset(d, 0x5a, bytes));
+  int ncu = 0; CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  const u32x4* p = (const u32x4*)d;
+  auto run = [&](const char* name, auto launch) {
+    for (int w = 0; w < 30; ++w) launch();
+    std::vector<float> ts;
+    for (int r = 0; r < 30; ++r) { CK(hipEventRecord(a)); launch(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b)); ts.push_back(ms); }
+    std::sort(ts.begin(), ts.end());
+    printf("%-48s med %.4f ms  %.1f GB/s (best %.1f)\n", name, ts[15], bytes / ts[15] / 1e6, bytes / ts[0] / 1e6); fflush(stdout);
+  };
+#define WA(R, NT, T) run("waitall R=" #R " nt=" #NT " T=" #T, [&] { hipLaunchKernelGGL((rd_waitall<R, NT>), dim3(ncu), dim3(T), 0, 0, p, n16, sink); });
+#define PP(R, NT, WC, T) run("pingpong R=" #R " nt=" #NT " wavecontig=" #WC " T=" #T, [&] { hipLaunchKernelGGL((rd_pingpong<R, NT, WC>), dim3(ncu), dim3(T), 0, 0, p, n16, sink); });
+  const uint64_t cbytes = 4294967296ull;  // seg: 4 GiB MR read, ~4.3 GB of frames written
+  uint8_t* d2; CK(hipMalloc(&d2, cbytes));
+  auto runc = [&](const char* name, auto launch) {
+    for (int w = 0; w < 10; ++w) launch();
+    std::vector<float> ts;
+    for (int r = 0; r < 15; ++r) { CK(hipEventRecord(a)); launch(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b)); ts.push_back(ms); }
+    std::sort(ts.begin(), ts.end());
+    printf("%-48s med %.4f ms  %.1f GB/s moved\n", name, ts[7], 2.0 * cbytes / ts[7] / 1e6); fflush(stdout);
+  };
+#define CP(R, NTS, T) runc("copy R=" #R " ntstore=" #NTS " T=" #T, [&] { hipLaunchKernelGGL((cp_waitall<R, NTS>), dim3(ncu), dim3(T), 0, 0, (const u32x4*)d, (u32x4*)d2, cbytes / 16); });
+  for (int rep = 0; rep < 2; ++rep) {
+    WA(8, true, 1024) WA(8, true, 512) WA(4, true, 1024) WA(16, true, 256) WA(8, true, 768) WA(4, true, 768)
+    CP(4, true, 1024) CP(4, true, 512) CP(8, true, 512) CP(8, true, 256) CP(4, true, 768) CP(2, true, 1024) CP(4, false, 512)
+  }
+  return 0;
+}
