@@ -649,6 +649,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
     // 256 B +5 %; a quarter or three quarters of the waves taking the long
     // sets, or claiming the next set before finishing the current one, were
     // no better.
+#ifdef RICRC_RAGGED_SORT_ONLY  // diagnostic build only: windows sorted, no set processed
+    if (nsets < 0)
+#endif
     for (;;) {
       uint32_t old = 0;
       if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? 0x10000u : 1u);

@@ -14,6 +14,7 @@ ROOT = Path(__file__).resolve().parent.parent
 ap = argparse.ArgumentParser()
 ap.add_argument("--workloads", default="cfg2")
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--bench-args", default="", help="extra bench.py arguments, e.g. '--lanes 16'")
 ap.add_argument("libs", nargs="+")
 args = ap.parse_args()
 for rnd in range(args.rounds):
@@ -21,7 +22,7 @@ for rnd in range(args.rounds):
         for lib in args.libs:
             env = dict(os.environ, ROCE_ICRC_LIB=str(Path(lib).resolve()))
             r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", wl,
-                                "--no-cpu-baseline", "--no-e2e"], env=env, timeout=300,
+                                "--no-cpu-baseline", "--no-e2e"] + args.bench_args.split(), env=env, timeout=300,
                                capture_output=True, text=True)
             if r.returncode != 0:
                 print(r.stderr[-2000:], flush=True)
