@@ -100,6 +100,33 @@ def test_uniform_4k_strided(engine, lanes):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("n", [1, 7, 257, 1283, 9001, 40003])
+def test_strided_batch_sizes_output_runs(engine, n):
+    """The strided kernel writes a workgroup's ICRC words as one run of
+    16-byte buffer stores plus a 4-byte remainder (round 2); tail sets
+    claimed from other workgroups write their own words.  Batch sizes that
+    leave every remainder length, at 1, 8 and 64 lanes, bit-exact and with
+    nothing written past the batch."""
+    buf, stride, flen = synth.uniform_frames(n, 512, seed=synth.SEED_CFG2 + n)
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    for lanes in (1, 8, 64):
+        engine.set_lanes(lanes)
+        try:
+            got, st = engine.compute_strided(buf, stride, flen, n)
+        finally:
+            engine.set_lanes(0)
+        assert (st == 0).all()
+        np.testing.assert_array_equal(got, want, err_msg=f"lanes {lanes}")
+    torch = pytest.importorskip("torch")
+    d = torch.from_numpy(buf).cuda()
+    out = torch.full((n + 64,), -1, dtype=torch.int32, device="cuda")  # sentinel tail
+    engine.compute_strided_dev(d, stride, flen, n, out)
+    torch.cuda.synchronize()
+    h = out.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(h[:n], want)
+    assert (h[n:] == 0xFFFFFFFF).all()
+
+
 @pytest.mark.parametrize("lanes", LANES)
 def test_mixed_mtu_compute_and_verify(engine, lanes):
     n = 5000
