@@ -257,6 +257,48 @@ struct Keys16 {
   }
 };
 
+// Keys8: 8 copies in the LOW half of 256-byte rows -- 32 KiB of tables in
+//   64 KiB of address space, the high 128 B of every row free for the
+//   caller.  addr(t, e, c) = e * 256 + t * 32 + c * 4, c = lane & 7.  The
+//   four 8-lane groups q = (lane >> 3) & 3 of a half-wave read table i ^ q
+//   (register byte i ^ q) in lookup i: bank (addr / 4) % 32 = 8 (i ^ q) + c,
+//   32 distinct banks.  One register holds the four row offsets
+//   (i ^ q) * 32 + c * 4 as bytes; lookup i's selector takes byte i ^ q of
+//   the CRC register to address byte 1 and byte i of that register to byte 0.
+struct Keys8 {
+  static constexpr uint32_t kHole = 128;  // free bytes [128, 256) of each of the 256 rows
+  uint32_t k;               // byte i: (i ^ q) * 32 + c * 4
+  uint32_t s0, s1, s2, s3;  // v_perm selectors
+  __device__ static Keys8 make(int lane) {
+    const uint32_t c = (uint32_t)(lane & 7), q = (uint32_t)(lane >> 3) & 3u;
+    Keys8 r;
+    r.k = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) r.k |= (((i ^ q) * 32u + c * 4u) << (8 * i));
+    r.s0 = 0x0C0C0000u | ((4u + (0u ^ q)) << 8) | 0u;
+    r.s1 = 0x0C0C0000u | ((4u + (1u ^ q)) << 8) | 1u;
+    r.s2 = 0x0C0C0000u | ((4u + (2u ^ q)) << 8) | 2u;
+    r.s3 = 0x0C0C0000u | ((4u + (3u ^ q)) << 8) | 3u;
+    return r;
+  }
+  template <int THREADS>
+  __device__ static void stage(const uint32_t* m, int tid) {
+    for (int i = tid; i < 2048; i += THREADS) {  // 1024 words x 2 quads of copies
+      const int w = i >> 1, h = i & 1;            // w = t * 256 + e
+      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m[w]);
+    }
+  }
+  __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
+    const uint32_t x = xor3(P, T, w);
+    const uint32_t a0 = __builtin_amdgcn_perm(x, k, s0);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, k, s1);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, k, s2);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, k, s3);
+    P = xor3(lds_rd(a0), lds_rd(a1), lds_rd(a2));
+    T = lds_rd(a3);
+  }
+};
+
 // The layout of the lane-group kernels (strided, ragged, segmentation).
 // Keys16 there (LDS-neutral for the 32x set's 64 KiB, larger ragged windows)
 // measured 2-4 % slower on mixed-MTU batches; the small kernel uses Keys16.

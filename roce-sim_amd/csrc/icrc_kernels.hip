@@ -696,15 +696,36 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 // the prefetch.  Hence unconditional LDS writes into the slot and the masks
 // applied in LDS rather than by uniform selects in the loop.
 //
-// LDS: [0, 64 KiB) Mul(128) in the Keys16 layout (icrc_device.hpp: 16
-// conflict-free copies, one v_perm_b32 per address), [64, 68 KiB) Mul(-32),
-// then one staging slot of 64 x stride bytes per wave.
+// LDS: [0, 64 KiB) Mul(128) in the Keys8 layout (icrc_device.hpp: 8
+// conflict-free copies in the low half of 256 rows of 256 B, one v_perm_b32
+// per address), then one staging slot of 64 x stride bytes per wave, the
+// output ring's tail, and Mul(-32) in the last 4 KiB.  The output ring
+// starts in the free high halves of the table rows (32 KiB) and continues
+// after the staging slots.
+// 12 waves (cfg5, 108-B frames: 8 waves 4975, 11 4899, 12 5034, 13 4773
+// GiB/s, 3 A/B rounds; an odd count leaves one SIMD a wave short, so the
+// launch rounds it down to even).  With Keys16 tables (64 KiB) and the ring
+// after the slots, 8 waves were best (6-10 waves: -10 % to -2.5 %); Keys8
+// (32 KiB of tables, the ring's head in the free row halves) gained +1.8 %
+// at 8 waves.
 #ifndef RICRC_SMALL_WAVES
-#define RICRC_SMALL_WAVES 8
+#define RICRC_SMALL_WAVES 12
 #endif
 constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
-constexpr uint32_t kSmallComb = Keys16::kComb;
-constexpr uint32_t kSmallStage = kSmallComb + 4096;
+using SmallKeys = Keys8;
+constexpr uint32_t kSmallComb = 163840u - 4096u;
+constexpr uint32_t kSmallStage = 65536;
+constexpr uint32_t kSmallHoleWords = 256u * (256u - Keys8::kHole) / 4u;  // ring words in the row halves
+// LDS byte address of ring word k / ring quad i (16 B): the row halves first,
+// then the tail after the staging slots
+__device__ __forceinline__ uint32_t small_ring_word(uint32_t tail, uint32_t k) {
+  return k < kSmallHoleWords ? (k >> 5) * 256u + Keys8::kHole + (k & 31u) * 4u
+                             : tail + 4u * (k - kSmallHoleWords);
+}
+__device__ __forceinline__ uint32_t small_ring_quad(uint32_t tail, uint32_t i) {
+  return i < kSmallHoleWords / 4u ? (i >> 3) * 256u + Keys8::kHole + (i & 7u) * 16u
+                                  : tail + 16u * (i - kSmallHoleWords / 4u);
+}
 constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + 3) / 4;  // ns <= 8
 #ifndef RICRC_SMALL_OUTBUF
 #define RICRC_SMALL_OUTBUF 64
@@ -733,16 +754,16 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   const int ns = (n + 3) >> 2, pad = 4 * ns - n;  // steps, zero dwords in front
   {
     const uint32_t* m128 = a.tables;  // main set 0: Mul(128)
-    for (int i = tid; i < 16384; i += (int)blockDim.x) {  // 16 copies of 1024 words
-      const int w = i >> 4, c = i & 15;  // w = t * 256 + e
-      lds_wr((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + c * 4), m128[w]);
+    for (int i = tid; i < 2048; i += (int)blockDim.x) {  // 8 copies of 1024 words, 2 quads
+      const int w = i >> 1, h = i & 1;  // w = t * 256 + e
+      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m128[w]);
     }
     const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
     for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallComb + 4u * i, cm32[i]);
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  const Keys16 kk = Keys16::make(lane);
+  const SmallKeys kk = SmallKeys::make(lane);
   const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch (<= 64 C)
   const uint32_t nw = blockDim.x >> 6;
   const uint32_t stage = kSmallStage + (uint32_t)wave * 64u * S;
@@ -773,8 +794,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   // contiguous run of 16-byte stores between two barriers, instead of each
   // wave storing 256 B per batch into the read stream.
   constexpr bool kRing = kSmallOutRounds > 0 && (OUTS & 1) != 0 && !VERIFY;
-  const uint32_t ring = kSmallStage + nw * 64u * S;
-  const uint32_t rounds_cap = kRing ? min((uint32_t)kSmallOutRounds, (163840u - ring) / (nw * 256u)) : 0u;
+  const uint32_t ring = kSmallStage + nw * 64u * S;  // the ring's tail (small_ring_word)
+  const uint32_t rounds_cap =
+      kRing ? min((uint32_t)kSmallOutRounds, (kSmallHoleWords + (kSmallComb - ring) / 4u) / (nw * 64u)) : 0u;
   uint32_t ring_base = 0;  // first packet of the ring's current window
   auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer,
                   bool to_ring = false) {
@@ -791,7 +813,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
 #else
       if constexpr ((OUTS & 1) != 0) {
         if (kRing && to_ring)
-          lds_wr(ring + 4u * (pkt - ring_base), icrc);
+          lds_wr(small_ring_word(ring, pkt - ring_base), icrc);
         else
           a.icrc_out[pkt] = icrc;
       }
@@ -899,7 +921,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       __builtin_amdgcn_s_barrier();
       const auto dst = out_rsrc(a.icrc_out + ring_base, 4u * words);
       for (uint32_t i = (uint32_t)tid; i < words / 4u; i += blockDim.x)
-        out_store128<kSmallOutPol>(*(const lds_u32x4*)(uintptr_t)(ring + 16u * i), dst, 16u * i);
+        out_store128<kSmallOutPol>(*(const lds_u32x4*)(uintptr_t)small_ring_quad(ring, i), dst, 16u * i);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // the ring is read before anyone writes it again
       __builtin_amdgcn_s_barrier();
       ring_base += in_ring * nw * 64u;
@@ -1068,7 +1090,8 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
   kernel_fn k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;
-  const uint32_t nw = min((uint32_t)kSmallMaxWaves, (163840u - kSmallStage) / slot);
+  uint32_t nw = min((uint32_t)kSmallMaxWaves, (kSmallComb - kSmallStage) / slot);
+  if (nw > 2 && (nw & 1u)) --nw;  // even: every SIMD the same number of waves
   const size_t lds = 163840;  // staging slots, then the output ring in what is left
   const uint64_t nb = (a.n + 63) / 64;
   uint64_t blocks = (nb + nw - 1) / nw;
