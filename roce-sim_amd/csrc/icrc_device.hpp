@@ -267,6 +267,7 @@ struct Keys16 {
 //   the CRC register to address byte 1 and byte i of that register to byte 0.
 struct Keys8 {
   static constexpr uint32_t kHole = 128;  // free bytes [128, 256) of each of the 256 rows
+  static constexpr uint32_t kComb = 65536;  // combine sets after the rows (lane-group kernels)
   uint32_t k;               // byte i: (i ^ q) * 32 + c * 4
   uint32_t s0, s1, s2, s3;  // v_perm selectors
   __device__ static Keys8 make(int lane) {
@@ -301,9 +302,14 @@ struct Keys8 {
 
 // The layout of the lane-group kernels (strided, ragged, segmentation).
 // Keys16 there (LDS-neutral for the 32x set's 64 KiB, larger ragged windows)
-// measured 2-4 % slower on mixed-MTU batches; the small kernel uses Keys16.
+// measured 2-4 % slower on mixed-MTU batches in round 1; round 2 on the
+// 12-wave build (2 A/B rounds): cfg2 equal with all three, cfg3 Keys8 -1.1 %
+// and Keys16 -1.8 % even with one sort window per workgroup.  The small
+// kernel uses Keys8.
 #ifdef RICRC_TABLES16
 using MainKeys = Keys16;
+#elif defined(RICRC_TABLES8)
+using MainKeys = Keys8;
 #else
 using MainKeys = Keys32;
 #endif
