@@ -494,6 +494,32 @@ def test_full_size_cfg5_small_bit_exact(engine):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
 
 
+@pytest.mark.parametrize("payload,stride", [(4, 48), (76, 128)])
+def test_small_kernel_ring_regions(engine, payload, stride):
+    """The small-frame kernel's output ring starts in the free halves of its
+    table rows and continues after the staging slots (round 2).  Batches
+    large enough that every workgroup's flushes run through both regions, at
+    the smallest stride (12 waves) and the largest (10 waves after rounding
+    to even, the largest per-wave slot), with a gap after each frame at 128:
+    every word against the C oracle, nothing written past the batch."""
+    torch = pytest.importorskip("torch")
+    n = 6_000_011  # > 256 workgroups x 2 full rings of 128-B frames
+    flen = 44 + payload
+    frames, s0, _ = synth.uniform_frames(n, payload, seed=synth.SEED_CFG5 + stride)
+    buf = np.zeros((n - 1) * stride + flen, np.uint8)
+    rows = np.lib.stride_tricks.as_strided(buf, (n, flen), (stride, 1))
+    rows[:] = frames.reshape(n, s0)[:, :flen]
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.full((n + 256,), -1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.compute_strided_dev(d, stride, flen, n, out, stream=s.cuda_stream)
+    s.synchronize()
+    h = out.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(h[:n], want)
+    assert (h[n:] == 0xFFFFFFFF).all()
+
+
 def test_ragged_many_windows_random_sizes(engine):
     """The ragged kernel over 2^21 frames of random length (44 .. 1020 B, so
     every workgroup sorts several windows and claims sets from both ends of
