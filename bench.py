@@ -486,9 +486,11 @@ def main():
     ceil_key, ceil_gbps, ceil_ts = ceiling()
     if os.environ.get("ROCE_ICRC_BENCH_TRACE"):  # per-launch times (us) to stderr
         us = lambda xs: [round(x * 1e6) for x in xs]  # noqa: E731
+        gap = wev[-1][1].elapsed_time(evs[0][0]) * 1e3 if wev and evs else -1.0
         print(f"[trace] rank {rank} ceiling n={len(ceil_ts)} {us(ceil_ts)}\n[trace] warmup "
-              f"{us([a.elapsed_time(b) * 1e-3 for a, b in wev])}\n[trace] timed {us(kern_s)}",
-              file=sys.stderr, flush=True)
+              f"{us([a.elapsed_time(b) * 1e-3 for a, b in wev])}\n[trace] timed {us(kern_s)}\n"
+              f"[trace] idle before the timed steps {gap:.1f} us, wall {t_local * 1e3:.3f} ms, "
+              f"kernels {sum(kern_s) * 1e3:.3f} ms", file=sys.stderr, flush=True)
     t = torch.tensor([t_local], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
