@@ -248,10 +248,19 @@ __device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
 
 // Where a block's ICRC words go: packets [p0, p0 + cap) into an LDS buffer
 // at kOutLds<LOG2G> (written out whole when the block is done), the rest
-// straight to icrc_out.  cap = 0: no buffer (ragged kernel).
+// straight to icrc_out.  cap = 0: no buffer.  Likewise the verify verdicts
+// of packets [ok_p0, ok_p0 + ok_cap) into LDS bytes at ok_lds (the ragged
+// kernel's window, written out at the window's end).
 struct OutBuf {
   uint32_t p0, cap;
+  uint32_t ok_p0 = 0, ok_cap = 0, ok_lds = 0;
 };
+__device__ __forceinline__ void lds_wr8(uint32_t byte_addr, uint32_t v) {
+  *(__attribute__((address_space(3))) uint8_t*)(uintptr_t)byte_addr = (uint8_t)v;
+}
+__device__ __forceinline__ uint32_t lds_rd8(uint32_t byte_addr) {
+  return *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)byte_addr;
+}
 template <int LOG2G>
 constexpr uint32_t kOutLds = kFixLut<LOG2G, MainKeys> + 256u;  // after the fix-up LUT
 
@@ -377,7 +386,11 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
     if constexpr (VERIFY) {
       const bool ok = good && trailer == icrc;
       if (good && !ok) st |= kPktIcrcMismatch;
-      stg8<kPktStorePol>(a.ok_out + p.pkt, ok ? 1u : 0u);
+      const uint32_t ko = p.pkt - ob.ok_p0;
+      if (ko < ob.ok_cap)
+        lds_wr8(ob.ok_lds + ko, ok ? 1u : 0u);
+      else
+        stg8<kPktStorePol>(a.ok_out + p.pkt, ok ? 1u : 0u);
     }
     if (a.icrc_out) {
       const uint32_t k = p.pkt - ob.p0;
@@ -538,11 +551,13 @@ struct RaggedLds {
   static constexpr uint32_t kHist = kBase;               // kBuckets x u32 counts / cursors
   static constexpr uint32_t kPerm = kBase + 4 * kBuckets;  // window x u16 local indices
   static constexpr int kAvail = (int)(163840u - kPerm);
-  // sorted descriptors: u16 local index, u32 offset / 4, u16 length (8 B)
-  static constexpr int kWindow = (kAvail / 8 >= 8192) ? 8192 : (kAvail / 8) / 64 * 64;
+  // sorted descriptors: u16 local index, u32 offset / 4, u16 length (8 B),
+  // then the window's verify verdicts (1 B, in packet order)
+  static constexpr int kWindow = (kAvail / 9 >= 8192) ? 8192 : (kAvail / 9) / 64 * 64;
   static constexpr uint32_t kRoff = kPerm + 2 * kWindow;
   static constexpr uint32_t kRlen = kRoff + 4 * kWindow;
-  static constexpr uint32_t kBytes = kRlen + 2 * kWindow;
+  static constexpr uint32_t kOk = kRlen + 2 * kWindow;
+  static constexpr uint32_t kBytes = kOk + kWindow;
 };
 
 template <int LOG2G, bool VERIFY>
@@ -649,6 +664,14 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
     // 256 B +5 %; a quarter or three quarters of the waves taking the long
     // sets, or claiming the next set before finishing the current one, were
     // no better.
+    // verify verdicts collect in LDS and leave as one run per window
+    // (written one by one into the read stream they cost 1.3 %, ablated)
+    OutBuf ob = {0, 0};
+    if constexpr (VERIFY) {
+      ob.ok_p0 = w0;
+      ob.ok_cap = (uint32_t)cnt;
+      ob.ok_lds = LD::kOk;
+    }
 #ifdef RICRC_RAGGED_SORT_ONLY  // diagnostic build only: windows sorted, no set processed
     if (nsets < 0)
 #endif
@@ -661,9 +684,12 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
       const int set = from_back ? nsets - 1 - bk : f;
       const Pkt p = make(set);
       Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
-      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk);
+      finish_packet<LOG2G, VERIFY>(a, p, b, gl, grp * G, kk, ob);
     }
     __syncthreads();
+    if constexpr (VERIFY) {  // the window's verdicts, one contiguous run
+      for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
+    }
   }
 #ifdef RICRC_BLOCK_TIMES
   if (tid == 0 && a.status_out) {
