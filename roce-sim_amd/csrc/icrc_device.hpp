@@ -265,17 +265,21 @@ struct Keys16 {
 //   32 distinct banks.  One register holds the four row offsets
 //   (i ^ q) * 32 + c * 4 as bytes; lookup i's selector takes byte i ^ q of
 //   the CRC register to address byte 1 and byte i of that register to byte 0.
-struct Keys8 {
-  static constexpr uint32_t kHole = 128;  // free bytes [128, 256) of each of the 256 rows
+// Keys8T<1> is the same layout in the HIGH halves of the rows (every row
+// offset + 128): two table sets share the 64 KiB (the mixed-width ragged
+// kernel holds Mul(1024) and Mul(512) there).
+template <int HALF>
+struct Keys8T {
+  static constexpr uint32_t kHole = 128;  // free bytes [128, 256) of each of the 256 rows (HALF 0)
   static constexpr uint32_t kComb = 65536;  // combine sets after the rows (lane-group kernels)
-  uint32_t k;               // byte i: (i ^ q) * 32 + c * 4
+  uint32_t k;               // byte i: (i ^ q) * 32 + c * 4 (+ 128 HALF)
   uint32_t s0, s1, s2, s3;  // v_perm selectors
-  __device__ static Keys8 make(int lane) {
+  __device__ static Keys8T make(int lane) {
     const uint32_t c = (uint32_t)(lane & 7), q = (uint32_t)(lane >> 3) & 3u;
-    Keys8 r;
+    Keys8T r;
     r.k = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) r.k |= (((i ^ q) * 32u + c * 4u) << (8 * i));
+    for (uint32_t i = 0; i < 4; ++i) r.k |= (((i ^ q) * 32u + c * 4u + 128u * HALF) << (8 * i));
     r.s0 = 0x0C0C0000u | ((4u + (0u ^ q)) << 8) | 0u;
     r.s1 = 0x0C0C0000u | ((4u + (1u ^ q)) << 8) | 1u;
     r.s2 = 0x0C0C0000u | ((4u + (2u ^ q)) << 8) | 2u;
@@ -286,7 +290,7 @@ struct Keys8 {
   __device__ static void stage(const uint32_t* m, int tid) {
     for (int i = tid; i < 2048; i += THREADS) {  // 1024 words x 2 quads of copies
       const int w = i >> 1, h = i & 1;            // w = t * 256 + e
-      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m[w]);
+      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128 * HALF), m[w]);
     }
   }
   __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
@@ -299,6 +303,7 @@ struct Keys8 {
     T = lds_rd(a3);
   }
 };
+using Keys8 = Keys8T<0>;
 
 // The layout of the lane-group kernels (strided, ragged, segmentation).
 // Keys16 there (LDS-neutral for the 32x set's 64 KiB, larger ragged windows)

@@ -193,9 +193,10 @@ __device__ __forceinline__ void fix_chunk(u32x4& w, int kb, int kub, int kbb, ui
 // Recomputation of one packet by its group with the masks of a general IHL
 // (IPv4 options), or of a frame at an unaligned start (byte loads).  Rare
 // path: the main loop applies the IHL-5 masks to dword-aligned frames.
-template <int LOG2G>
-__device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, MainKeys kk) {
+template <int LOG2G, class K>
+__device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base) {
   constexpr int G = 1 << LOG2G;
+  const K kk = K::make(__lane_id());  // (rebuilt here: no key registers passed on the stack)
   constexpr int DPI = 4 * G;
   const int kub = ihl + 1, kbb = ihl + 3;
   Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -209,8 +210,8 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base, M
     else
       fold(A, w, kk);
   }
-  return combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
-                                  A.P[3] ^ A.T[3], p.r, gl, base);
+  return combine<LOG2G, K>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2], A.P[3] ^ A.T[3],
+                           p.r, gl, base);
 }
 
 
@@ -264,10 +265,12 @@ __device__ __forceinline__ uint32_t lds_rd8(uint32_t byte_addr) {
 template <int LOG2G>
 constexpr uint32_t kOutLds = kFixLut<LOG2G, MainKeys> + 256u;  // after the fix-up LUT
 
-template <int LOG2G, bool VERIFY>
+// K: the table layout (MainKeys, or Keys8T in the mixed-width ragged
+// kernel); LUT: LDS address of the IHL-5 fix-up table.
+template <int LOG2G, bool VERIFY, class K, uint32_t LUT>
 __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
-                                            int base, const MainKeys& kk, OutBuf ob);
+                                            int base, const K& kk, OutBuf ob);
 
 // A wave issues its next body block's loads (lane-group kernels) or its next
 // batch's prefetch (small-frame kernel) at raised priority, so the sequencer
@@ -286,14 +289,14 @@ __device__ __forceinline__ void body_prio_lo() {
 }
 
 // Fold, combine, check and emit one packet whose first batch is in `b`.
-template <int LOG2G, bool VERIFY>
+template <int LOG2G, bool VERIFY, class K = MainKeys, uint32_t LUT = kFixLut<LOG2G, MainKeys>>
 __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, Batch<kUnroll>& b,
-                                              int gl, int base, const MainKeys& kk,
+                                              int gl, int base, const K& kk,
                                               OutBuf ob = {0, 0}) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
   constexpr int U = kUnroll;
-  constexpr uint32_t kLut = kFixLut<LOG2G, MainKeys>;
+  constexpr uint32_t kLut = LUT;
   // Iterations: head [0, jhh) with the fix-ups, body [jhh, J-1) in blocks of
   // U (the first block holds the remainder), then the last one (J-1), which
   // skips columns past the end and may also need the fix-ups.
@@ -342,18 +345,18 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
     if (JL < p.jh) fix_chunk5(w, kb, kLut, h0, h2);
     fold_last(A, w, kb, p.n, kk);
   }
-  emit_packet<LOG2G, VERIFY>(a, p, A, h0, h2, b.trailer, gl, base, kk, ob);
+  emit_packet<LOG2G, VERIFY, K, LUT>(a, p, A, h0, h2, b.trailer, gl, base, kk, ob);
 }
 
 // Packet done: fold the group's columns, check the header, emit.
-template <int LOG2G, bool VERIFY>
+template <int LOG2G, bool VERIFY, class K, uint32_t LUT>
 __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, const Col& A,
                                             uint32_t h0, uint32_t h2, uint32_t trailer, int gl,
-                                            int base, const MainKeys& kk, OutBuf ob) {
+                                            int base, const K& kk, OutBuf ob) {
   constexpr int G = 1 << LOG2G;
   constexpr int DPI = 4 * G;
-  uint32_t B = combine<LOG2G, MainKeys>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
-                                        A.P[3] ^ A.T[3], p.r, gl, base);
+  uint32_t B = combine<LOG2G, K>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                 A.P[3] ^ A.T[3], p.r, gl, base);
   uint32_t d0 = (uint32_t)__shfl((int)h0, base + (p.S >> 2), 64);
   uint32_t d2 = (uint32_t)__shfl((int)h2, base + (((p.S + 2) & (DPI - 1)) >> 2), 64);
   if (p.unal) {  // (per group) frame at an unaligned start: header bytes read directly
@@ -375,8 +378,8 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
   }
   const bool good = (st & kPktFatal) == 0;
   if (good && (ihl != 5 || p.unal))
-    B = slow_packet<LOG2G>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl, gl,
-                           base, kk);
+    B = slow_packet<LOG2G, K>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl, gl,
+                              base);
   const uint32_t icrc = good ? ~B : 0u;
 #ifdef RICRC_ABLATE_OUT  // diagnostic build only: per-packet output stores removed (kept live)
   if (p.live && gl == 0 && icrc == 0x9E3779B9u) {
@@ -543,22 +546,23 @@ __global__ void __launch_bounds__(kStridedThreads, 1) icrc_strided_kernel(IcrcAr
 // Each workgroup therefore takes a contiguous window of packets (locality
 // kept) and counting-sorts it in LDS by iteration count; waves then claim
 // size-homogeneous sets of the sorted window from both ends.
-template <int LOG2G>
-struct RaggedLds {
-  static constexpr int kNComb = 1 + LOG2G;
-  static constexpr uint32_t kBase = kFixLut<LOG2G, MainKeys> + 256u;  // after the fix-up LUT
+template <uint32_t BASE, int CAP = 8192>
+struct WindowLds {
+  static constexpr uint32_t kBase = BASE;  // after the tables and the fix-up LUT
   static constexpr int kBuckets = 128;
   static constexpr uint32_t kHist = kBase;               // kBuckets x u32 counts / cursors
   static constexpr uint32_t kPerm = kBase + 4 * kBuckets;  // window x u16 local indices
   static constexpr int kAvail = (int)(163840u - kPerm);
   // sorted descriptors: u16 local index, u32 offset / 4, u16 length (8 B),
   // then the window's verify verdicts (1 B, in packet order)
-  static constexpr int kWindow = (kAvail / 9 >= 8192) ? 8192 : (kAvail / 9) / 64 * 64;
+  static constexpr int kWindow = (kAvail / 9 >= CAP) ? CAP : (kAvail / 9) / 64 * 64;
   static constexpr uint32_t kRoff = kPerm + 2 * kWindow;
   static constexpr uint32_t kRlen = kRoff + 4 * kWindow;
   static constexpr uint32_t kOk = kRlen + 2 * kWindow;
   static constexpr uint32_t kBytes = kOk + kWindow;
 };
+template <int LOG2G>
+using RaggedLds = WindowLds<kFixLut<LOG2G, MainKeys> + 256u>;
 
 template <int LOG2G, bool VERIFY>
 __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a) {
@@ -697,6 +701,203 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
     ((uint64_t*)a.status_out)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Mixed-width ragged kernel (the G = 8 choice for ragged batches).
+//
+// Short frames are instruction-bound in a lane group: at 256-B MTU a G = 8
+// set spends ~90 % of its instructions on per-packet work (describe, head
+// fix-ups, rotation, combine) that every lane of the group pays.  Halving the
+// group halves that cost per packet, while long frames need G = 8 for whole
+// 128-B lines per group load.  This kernel holds both table sets -- Mul(1024)
+// for G = 8 and Mul(512) for G = 4, in the two halves of the Keys8 rows (64
+// KiB together, icrc_device.hpp) -- and picks the width per set of the sorted
+// window: the front waves claim 16 packets from the short end and run them as
+// ONE G = 4 set when the claim's longest frame is short, else as two G = 8
+// sets; the back waves claim 8 from the long end at G = 8.  The combine sets
+// Mul(-32), Mul(-128 * 2^l) (l < 3) serve both widths.  The tables take 80 KiB
+// instead of 144, so a window holds up to 8192 packets (one window per
+// workgroup at cfg3).
+//
+// Claims are packets on the packed front | back << 16 counter.  A front claim
+// at (f, bk) owns [f, min(f + 16, cnt - bk)); a back claim owns
+// [max(cnt - bk - 8, f), cnt - bk): each side sees the other's position at
+// its own atomic, so the ranges are disjoint.
+#ifndef RICRC_RAGGED_MIXED
+#define RICRC_RAGGED_MIXED 1
+#endif
+// Frames of at most this many bytes (the claim's last, i.e. longest, sorted
+// frame) run as G = 4 sets.
+#ifndef RICRC_MIXED_SHORT_LEN
+#define RICRC_MIXED_SHORT_LEN 600
+#endif
+constexpr uint32_t kMixedShortLen = RICRC_MIXED_SHORT_LEN;
+using MixedKeysL = Keys8T<0>;  // Mul(1024), G = 8
+using MixedKeysS = Keys8T<1>;  // Mul(512), G = 4
+constexpr uint32_t kMixedLut = kFixLut<3, MixedKeysL>;  // after the 4 combine sets
+#ifndef RICRC_MIXED_WINDOW
+#define RICRC_MIXED_WINDOW 8192
+#endif
+using MixedLds = WindowLds<kMixedLut + 256u, RICRC_MIXED_WINDOW>;
+
+template <int LOG2G, bool VERIFY, class K>
+__device__ __forceinline__ void mixed_set(const IcrcArgs& a, int s, int e, uint32_t w0, int lane,
+                                          const OutBuf& ob) {
+  constexpr int G = 1 << LOG2G;
+  constexpr int DPI = 4 * G;
+  using LD = MixedLds;
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  const lds_u16* perm = (const lds_u16*)(uintptr_t)LD::kPerm;
+  const lds_u32* roff = (const lds_u32*)(uintptr_t)LD::kRoff;
+  const lds_u16* rlen = (const lds_u16*)(uintptr_t)LD::kRlen;
+  // the lane's per-width constants are rebuilt per set (an opaque copy of the
+  // lane id), not hoisted out of the claim loop: registers held for one width
+  // would be taken from the other's loads in flight
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  const int gl = ln & (G - 1), grp = ln >> LOG2G;
+  const K kk = K::make(ln);
+  const int idx = s + grp;
+  const bool live = idx < e;
+  const int ix = live ? idx : s;
+  const uint32_t pkt = w0 + perm[ix], ow = roff[ix];
+  const uint64_t off = ow != 0xFFFFFFFFu ? (uint64_t)ow << 2 : a.offsets[pkt];
+  const Pkt p = describe<DPI>(a.frames, pkt, live, live ? off : 0, live ? (uint32_t)rlen[ix] : 0);
+  Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+  finish_packet<LOG2G, VERIFY, K, kMixedLut>(a, p, b, gl, grp * G, kk, ob);
+}
+
+template <bool VERIFY>
+__global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(IcrcArgs a) {
+  constexpr int DPI = 32;  // sort key: G = 8 iterations
+  using LD = MixedLds;
+  constexpr int W = LD::kWindow;
+  constexpr int NB = LD::kBuckets;
+  static_assert(W + 16 < 65536, "claims are 16-bit counters");
+  const int tid = threadIdx.x;
+  stage_tables<3, kIcrcThreads, MixedKeysL>(a.tables, tid);
+  MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
+
+  const int lane = tid & 63;
+  const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
+  const uint32_t p0 = blockIdx.x * per_block;
+  const uint32_t p1 = min(a.n, p0 + per_block);
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  lds_u32* hist = (lds_u32*)(uintptr_t)LD::kHist;
+  lds_u16* perm = (lds_u16*)(uintptr_t)LD::kPerm;
+  lds_u32* roff = (lds_u32*)(uintptr_t)LD::kRoff;
+  lds_u16* rlen = (lds_u16*)(uintptr_t)LD::kRlen;
+  constexpr uint32_t kNoOff = 0xFFFFFFFFu;
+  lds_u32* claim = (lds_u32*)(uintptr_t)(LD::kBase - 4u);  // (free word at the end of the LUT)
+  const bool from_back = ((tid >> 6) & 1) != 0;
+
+  const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
+  const uint32_t wsz = p1 > p0 ? (p1 - p0 + nwin - 1) / nwin : 1;
+  for (uint32_t w0 = p0; w0 < p1; w0 += wsz) {
+    const int cnt = (int)min(wsz, p1 - w0);
+    if (tid < NB) hist[tid] = 0;
+    if (tid == NB) *claim = 0;
+    __syncthreads();
+    constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
+    int keys[KR];
+    uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const int i = tid + r * kIcrcThreads;
+      int key = 0;
+      offw[r] = kNoOff;
+      lw[r] = 0;
+      if (i < cnt) {
+        const uint32_t L = a.lens[w0 + i];
+        const uint64_t off = a.offsets[w0 + i];
+        if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
+        lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
+        if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
+          const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
+          key = min(NB - 1, (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
+        }
+        atomicAdd((uint32_t*)&hist[key], 1u);
+      }
+      keys[r] = key;
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of NB = 128 counts by one wave (2 per lane)
+      const uint32_t c0 = hist[2 * tid], c1 = hist[2 * tid + 1];
+      uint32_t s = c0 + c1;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)s, d, 64);
+        if (tid >= d) s += t;
+      }
+      const uint32_t excl = s - c0 - c1;
+      hist[2 * tid] = excl;
+      hist[2 * tid + 1] = excl + c0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const int i = tid + r * kIcrcThreads;
+      if (i < cnt) {
+        const uint32_t pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
+        perm[pos] = (uint16_t)i;
+        roff[pos] = offw[r];
+        rlen[pos] = (uint16_t)lw[r];
+      }
+    }
+    __syncthreads();
+    OutBuf ob = {0, 0};
+    if constexpr (VERIFY) {
+      ob.ok_p0 = w0;
+      ob.ok_cap = (uint32_t)cnt;
+      ob.ok_lds = LD::kOk;
+    }
+    // Claim size: 16 packets while the frames at this wave's end of the window
+    // are short, else 8.  Decided from the window's first 16 / last frame, then
+    // from the wave's own previous claim (the front end only grows longer, the
+    // back end only shorter), so a claim costs one LDS atomic.
+    uint32_t size = (uint32_t)__builtin_amdgcn_readfirstlane(
+                        (int)rlen[from_back ? cnt - 1 : min(15, cnt - 1)]) <= kMixedShortLen
+                        ? 16u : 8u;
+    for (;;) {
+      uint32_t old = 0;
+      if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? (size << 16) : size);
+      old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+      const int f = (int)(old & 0xFFFFu), bk = (int)(old >> 16);
+      if (f + bk >= cnt) break;
+      // the claim [s, e): 16 packets run as one G = 4 set if the longest
+      // (sorted last) is short, else as G = 8 sets of 8
+      int s, e;
+      if (from_back) {
+        e = cnt - bk;
+        s = max(e - (int)size, f);
+      } else {
+        s = f;
+        e = min(f + (int)size, cnt - bk);
+      }
+      if (size == 16u) {
+        const uint32_t longest = (uint32_t)__builtin_amdgcn_readfirstlane((int)rlen[e - 1]);
+        if (longest <= kMixedShortLen) {
+          mixed_set<2, VERIFY, MixedKeysS>(a, s, e, w0, lane, ob);
+          continue;
+        }
+        if (!from_back) size = 8u;  // the front has reached long frames
+        if (e - s > 8) {
+          mixed_set<3, VERIFY, MixedKeysL>(a, s, e - 8, w0, lane, ob);
+          s = e - 8;
+        }
+        mixed_set<3, VERIFY, MixedKeysL>(a, s, e, w0, lane, ob);
+      } else {
+        const uint32_t shortest = from_back ? rlen[s] : 0xFFFFu;  // (used after the set)
+        mixed_set<3, VERIFY, MixedKeysL>(a, s, e, w0, lane, ob);
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)shortest) <= kMixedShortLen) size = 16u;
+      }
+    }
+    __syncthreads();
+    if constexpr (VERIFY) {  // the window's verdicts, one contiguous run
+      for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1021,6 +1222,8 @@ typedef void (*kernel_fn)(IcrcArgs);
 
 template <int LOG2G>
 kernel_fn pick(bool ragged, bool verify) {
+  if (ragged && LOG2G == 3 && RICRC_RAGGED_MIXED)
+    return verify ? icrc_ragged_mixed_kernel<true> : icrc_ragged_mixed_kernel<false>;
   if (ragged) return verify ? icrc_ragged_kernel<LOG2G, true> : icrc_ragged_kernel<LOG2G, false>;
   return verify ? icrc_strided_kernel<LOG2G, true> : icrc_strided_kernel<LOG2G, false>;
 }
@@ -1044,7 +1247,7 @@ size_t lds_bytes(int log2g, bool ragged) {
     case 0: return RaggedLds<0>::kBytes;
     case 1: return RaggedLds<1>::kBytes;
     case 2: return RaggedLds<2>::kBytes;
-    case 3: return RaggedLds<3>::kBytes;
+    case 3: return RICRC_RAGGED_MIXED ? MixedLds::kBytes : RaggedLds<3>::kBytes;
     case 4: return RaggedLds<4>::kBytes;
     case 5: return RaggedLds<5>::kBytes;
     default: return RaggedLds<6>::kBytes;

@@ -41,7 +41,7 @@ else
   # the STREAM-read kernel reads the whole frame buffer: covered bytes + 4 B per frame
   BUF=$(python3 -c "import json; d=json.load(open('$OUT/bench_$TAG.json')); c=d['config']; print((c['covered_bytes_per_gpu'] + 4 * c['packets_per_gpu']) // 16 * 16)")
   KN=::icrc_
-  [ "$WL" = cfg3 ] && KN=", true>"  # the verify kernel (the compute launch in setup fills trailers)
+  [ "$WL" = cfg3 ] && KN="true>(ricrc::IcrcArgs"  # the verify kernel, either ragged form (the compute launch in setup fills trailers)
   python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
     --packets $NP --frame-bytes 0 --ceiling-read-bytes $BUF --alg-bytes $ALG --kernel "$KN" \
     --out $OUT/pmc_traffic_${TAG}_$WL.json || exit 1

@@ -521,15 +521,17 @@ def test_small_kernel_ring_regions(engine, payload, stride):
 
 
 def test_ragged_many_windows_random_sizes(engine):
-    """The ragged kernel over 2^21 frames of random length (44 .. 1020 B, so
-    every workgroup sorts several windows and claims sets from both ends of
-    each), laid out in memory order with malformed frames scattered in:
-    lengths not a multiple of 4, TCP instead of UDP, an IP total length that
-    disagrees with the frame, IPv4 options.  Lane settings 4, 8 and 16;
-    compute and verify against the C oracle."""
+    """The ragged kernels over 3 x 2^20 frames of random length (44 .. 1020 B,
+    so every workgroup sorts several windows -- two of 6144 in the
+    mixed-width kernel, whose windows hold up to 8192 -- and claims sets from
+    both ends of each), laid out in memory order with malformed frames
+    scattered in: lengths not a multiple of 4, TCP instead of UDP, an IP total
+    length that disagrees with the frame, IPv4 options.  Lane settings 4, 8
+    (the mixed-width kernel: G = 4 and G = 8 sets) and 16; compute and verify
+    against the C oracle."""
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(2024)
-    n = 1 << 21
+    n = 3 << 20
     lens = (rng.integers(11, 256, n) * 4).astype(np.uint32)
     offs = np.zeros(n, np.uint64)
     np.cumsum(lens[:-1], out=offs[1:])
@@ -582,7 +584,7 @@ def test_ragged_many_windows_random_sizes(engine):
         assert (got[odd] == 0).all()
         exp_ok = ok_want.astype(bool) & ~fatal
         np.testing.assert_array_equal(okh, exp_ok, err_msg=f"lanes {lanes}")
-        assert not okh[flip].any() and okh.sum() > n - 4000
+        assert not okh[flip].any() and okh.sum() > n - 5000
 
 
 def test_offsets_above_16_gib(engine):
