@@ -102,9 +102,14 @@ int pick_log2g(const ricrc_ctx* c, uint32_t typical_len) {
 // pay off: one notch more lanes than a uniform batch of the same mean length
 // (mixed-MTU mean 1.6 KiB -> G = 8, measured best).  Device-resident ragged
 // calls do not know the lengths on the host: they use the mixed-MTU choice.
+// Host batches of tiny frames (ACKs, 48 B) run best one lane per packet:
+// ragged 48-B frames G = 1 1655, G = 2 1351, G = 4 875 GiB/s (MI355X,
+// scripts/explore.py u4); at 300 B G = 4 / 8 lead (3130 / 3155).
 constexpr uint32_t kRaggedTypicalLen = 1632;
+constexpr uint32_t kRaggedTinyLen = 128;
 int ragged_log2g(const ricrc_ctx* c, uint32_t mean) {
   if (c->lanes > 0) return log2_lanes(c->lanes);
+  if (mean <= kRaggedTinyLen) return 0;
   const int l = auto_log2g(mean) + 1;
   return l > 4 ? 4 : l;
 }

@@ -587,6 +587,48 @@ def test_ragged_many_windows_random_sizes(engine):
         assert not okh[flip].any() and okh.sum() > n - 5000
 
 
+@pytest.mark.parametrize("mtus,n", [
+    ((548, 552, 556, 560, 564, 568), 200_003),   # frames 592 .. 612 B: the width boundary (600 B)
+    ((4, 4096), 100_001),                          # tiny and 4-KiB frames alternate in memory
+    ((8,) * 15 + (4096,), 300_007),               # one long frame per 16 short ones
+    ((256, 512, 1024, 2048, 4096), 2_200_009),    # cfg3 mix, two windows per workgroup
+])
+def test_mixed_width_claims(engine, mtus, n):
+    """The mixed-width ragged kernel (the lanes-8 / device-resident default):
+    claims of 16 short sorted frames run as one G = 4 set, the rest as G = 8
+    sets of 8, from both ends of every window.  Compositions that put the
+    600-B width boundary inside claims, alternate tiny and 4-KiB frames, or
+    hold one long frame per 16 short ones, with batch sizes that leave
+    partial claims where the two ends meet; compute and verify against the C
+    oracle (every 101st frame's payload corrupted for verify)."""
+    torch = pytest.importorskip("torch")
+    buf, offs, lens = synth.mixed_mtu_frames(n, mtus=mtus, seed=n)
+    want, _ = oracle_batch(buf, offsets=offs, lens=lens)
+    s = torch.cuda.current_stream()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    engine.set_lanes(8)
+    try:
+        d = torch.from_numpy(buf).cuda()
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        engine.compute_batch_dev(d, do, dl, n, out, stream=s.cuda_stream)
+        s.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+        trail = offs.astype(np.int64) + lens.astype(np.int64) - 4
+        buf[(trail[:, None] + np.arange(4)[None, :]).reshape(-1)] = want.view(np.uint8)
+        bad = np.arange(3, n, 101)
+        buf[offs[bad].astype(np.int64) + 41] ^= 0x10
+        d = torch.from_numpy(buf).cuda()
+        ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        engine.verify_batch_dev(d, do, dl, n, ok, stream=s.cuda_stream)
+        s.synchronize()
+    finally:
+        engine.set_lanes(0)
+    expect = np.ones(n, bool)
+    expect[bad] = False
+    np.testing.assert_array_equal(ok.cpu().numpy().astype(bool), expect)
+
+
 def test_offsets_above_16_gib(engine):
     """Frames placed beyond 2^34 bytes into one 17-GiB device buffer.  The
     ragged kernel keeps sorted offsets as u32 dwords (< 16 GiB) and takes a
