@@ -185,7 +185,22 @@ class Strided:
         return self.eng.lanes_for_len(self.flen)
 
     def check(self):
-        return {}
+        # self-consistency on the device (the bit-exact parity against the
+        # oracle is the cpu_baseline leg's and the test suite's): the words of
+        # the last step written into the trailers must all verify, and a frame
+        # with one payload bit flipped must not.  The frames are restored from
+        # the host copy by the host-inclusive leg that follows.
+        torch, n, S, L = self.torch, self.n, self.stride, self.flen
+        rows = self.d_frames[:n * S].view(n, S)
+        rows[:, L - 4:L] = self.out.view(torch.uint8).view(n, 4)
+        mid = n // 2
+        rows[mid, L - 8] = rows[mid, L - 8] ^ 1  # last payload dword (covered, unmasked)
+        ok = torch.zeros(n, dtype=torch.uint8, device=self.d_frames.device)
+        self.eng.verify_strided_dev(self.d_frames, S, L, n, ok)
+        okh = ok.cpu().numpy().astype(bool)
+        good = int(okh.sum())
+        return {"words_verified": good, "frames": n, "flipped_frame_fails": bool(not okh[mid]),
+                "pass": bool(good == n - 1 and not okh[mid])}
 
 
 class RaggedVerify:
@@ -251,7 +266,8 @@ class RaggedVerify:
                 "faults": {"icrc": int((fault == E.FAULT_ICRC).sum()),
                            "payload": int((fault == E.FAULT_PAYLOAD).sum()),
                            "masked": int((fault == E.FAULT_MASKED).sum())},
-                "verdict_matches_injected": bool((ok == expect).all())}
+                "verdict_matches_injected": bool((ok == expect).all()),
+                "pass": bool((ok == expect).all())}
 
 
 SEG_MSG = 256 * 1024
@@ -374,8 +390,9 @@ class Segment:
         ok = torch.empty(self.n, dtype=torch.uint8, device=dev)
         self.eng.verify_batch_dev(self.d_frames, offs, self.d_lens, self.n, ok)
         torch.cuda.synchronize()
-        return {"frames_verified": int(ok.sum()), "frames": self.n,
-                "lens_ok": bool((self.d_lens > 0).all())}
+        nv, lens_ok = int(ok.sum()), bool((self.d_lens > 0).all())
+        return {"frames_verified": nv, "frames": self.n, "lens_ok": lens_ok,
+                "pass": bool(nv == self.n and lens_ok)}
 
 
 CEIL_MIN_S = float(os.environ.get("ROCE_ICRC_CEIL_S", "0.08"))  # ceiling series length (s)
@@ -580,9 +597,15 @@ def main():
         if checks:
             line["checks"] = checks
         print(json.dumps(line), flush=True)
+    failed = [k for k, bad in (("checks", checks and not checks.get("pass", True)),
+                                ("cpu parity", bool(cpu and cpu.get("parity_mismatches_vs_gpu"))))
+              if bad]
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if failed:  # a fast wrong answer is not a result: fail loudly
+        print(f"bench: rank {rank}: {', '.join(failed)} FAILED: {checks}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":
