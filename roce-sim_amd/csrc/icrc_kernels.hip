@@ -733,6 +733,11 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 #define RICRC_MIXED_SHORT_LEN 600
 #endif
 constexpr uint32_t kMixedShortLen = RICRC_MIXED_SHORT_LEN;
+// Ragged launches: workgroups per CU over the whole launch (one resident at a
+// time: the LDS holds one); more than one lets the dispatcher balance CUs.
+#ifndef RICRC_RAGGED_BLOCKS_PER_CU
+#define RICRC_RAGGED_BLOCKS_PER_CU 1
+#endif
 using MixedKeysL = Keys8T<0>;  // Mul(1024), G = 8
 using MixedKeysS = Keys8T<1>;  // Mul(512), G = 4
 constexpr uint32_t kMixedLut = kFixLut<3, MixedKeysL>;  // after the 4 combine sets
@@ -859,6 +864,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     uint32_t size = (uint32_t)__builtin_amdgcn_readfirstlane(
                         (int)rlen[from_back ? cnt - 1 : min(15, cnt - 1)]) <= kMixedShortLen
                         ? 16u : 8u;
+#ifdef RICRC_RAGGED_SORT_ONLY  // diagnostic build only: windows sorted, no set processed
+    if (cnt < 0)
+#endif
     for (;;) {
       uint32_t old = 0;
       if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? (size << 16) : size);
@@ -1306,7 +1314,8 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   const uint64_t nsets = (a.n + ppw - 1) / ppw;
   const int waves = ragged ? kIcrcWaves : kStridedWaves;
   uint64_t blocks = (nsets + waves - 1) / waves;
-  if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
+  const uint64_t cap = (uint64_t)num_cus * (ragged ? RICRC_RAGGED_BLOCKS_PER_CU : 1);
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * waves), lds_bytes(log2g, ragged), stream, a);
   return hipGetLastError();

@@ -24,9 +24,12 @@ for rnd in range(args.rounds):
             r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", wl,
                                 "--no-cpu-baseline", "--no-e2e"] + args.bench_args.split(), env=env, timeout=300,
                                capture_output=True, text=True)
-            if r.returncode != 0:
+            # exit status 3: the line was printed but a check failed (diagnostic
+            # builds that skip work do that); anything else is an error
+            if r.returncode not in (0, 3):
                 print(r.stderr[-2000:], flush=True)
                 sys.exit(r.returncode)
             d = json.loads(r.stdout.strip().splitlines()[-1])
             print(f"r{rnd} {wl:5s} {Path(lib).name:12s} {d['value']:9.1f} GiB/s "
-                  f"kernel {d['kernel_ms_mean']:.4f} ms frac {d['roofline']['frac']}", flush=True)
+                  f"kernel {d['kernel_ms_mean']:.4f} ms frac {d['roofline']['frac']}"
+                  + ("" if r.returncode == 0 else "  (CHECK FAILED)"), flush=True)
