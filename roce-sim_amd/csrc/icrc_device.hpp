@@ -33,6 +33,23 @@ __device__ __forceinline__ void lds_wr4(uint32_t byte_addr, uint32_t v) {
   *(lds_u32x4*)(uintptr_t)byte_addr = u32x4{v, v, v, v};
 }
 
+// LDS staging of COUNT words: every global load of the thread is issued
+// before its first LDS write, so the copy costs one memory round trip.  (As
+// plain loops -- a guarded load, then the write -- the compiler waited for
+// each load in turn: a few microseconds of every launch's prologue.)
+template <int COUNT, int THREADS, class Load, class Store>
+__device__ __forceinline__ void stage_batched(int tid, Load ld, Store st) {
+  constexpr int R = (COUNT + THREADS - 1) / THREADS;
+  uint32_t v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = ld(min(tid + r * THREADS, COUNT - 1));
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = tid + r * THREADS;
+    if (COUNT % THREADS == 0 || i < COUNT) st(i, v[r]);
+  }
+}
+
 __device__ __forceinline__ uint32_t ldg32(const uint8_t* p) {
   return *(const uint32_t*)p;
 }
@@ -205,13 +222,12 @@ struct Keys32 {
   }
   template <int THREADS>
   __device__ static void stage(const uint32_t* m, int tid) {
-#pragma unroll
-    for (int r = 0; r < (8192 + THREADS - 1) / THREADS; ++r) {
-      const int i = tid + r * THREADS;  // 8192 16-byte quads
-      if (8192 % THREADS != 0 && i >= 8192) break;
-      const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
-      lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), m[tab * 256 + e]);
-    }
+    stage_batched<8192, THREADS>(  // 8192 16-byte quads
+        tid, [&](int i) { return m[(i >> 11) * 256 + ((i >> 3) & 255)]; },
+        [&](int i, uint32_t v) {
+          const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
+          lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), v);
+        });
   }
   __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
     const uint32_t x = xor3(P, T, w);
@@ -241,10 +257,12 @@ struct Keys16 {
   }
   template <int THREADS>
   __device__ static void stage(const uint32_t* m, int tid) {
-    for (int i = tid; i < 4096; i += THREADS) {  // 1024 words x 4 quads of copies
-      const int w = i >> 2, q = i & 3;           // w = t * 256 + e
-      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + q * 16), m[w]);
-    }
+    stage_batched<4096, THREADS>(  // 1024 words x 4 quads of copies, w = t * 256 + e
+        tid, [&](int i) { return m[i >> 2]; },
+        [&](int i, uint32_t v) {
+          const int w = i >> 2, q = i & 3;
+          lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 64 + q * 16), v);
+        });
   }
   __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
     const uint32_t x = xor3(P, T, w);
@@ -288,10 +306,12 @@ struct Keys8T {
   }
   template <int THREADS>
   __device__ static void stage(const uint32_t* m, int tid) {
-    for (int i = tid; i < 2048; i += THREADS) {  // 1024 words x 2 quads of copies
-      const int w = i >> 1, h = i & 1;            // w = t * 256 + e
-      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128 * HALF), m[w]);
-    }
+    stage_batched<2048, THREADS>(  // 1024 words x 2 quads of copies, w = t * 256 + e
+        tid, [&](int i) { return m[i >> 1]; },
+        [&](int i, uint32_t v) {
+          const int w = i >> 1, h = i & 1;
+          lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128 * HALF), v);
+        });
   }
   __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
     const uint32_t x = xor3(P, T, w);
@@ -358,7 +378,8 @@ __device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
   constexpr int NCOMB = 1 + LOG2G;
   K::template stage<THREADS>(tables + LOG2G * 1024, tid);
   const uint32_t* gc = tables + kNumMainSets * 1024;
-  for (int i = tid; i < NCOMB * 1024; i += THREADS) lds_wr(K::kComb + 4u * i, gc[i]);
+  stage_batched<NCOMB * 1024, THREADS>(
+      tid, [&](int i) { return gc[i]; }, [&](int i, uint32_t v) { lds_wr(K::kComb + 4u * i, v); });
   if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
     const int k = tid - 3;
     const uint32_t lut = kFixLut<LOG2G, K>;

@@ -607,6 +607,16 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
     constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
     int keys[KR];
     uint32_t offw[KR], lw[KR];
+    // every descriptor load of the thread first (clamped, unconditional: a
+    // guarded load makes the compiler wait for each in turn), then the keys
+    uint32_t Lr[KR];
+    uint64_t Or[KR];
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const int ic = min(tid + r * kIcrcThreads, cnt - 1);
+      Lr[r] = a.lens[w0 + ic];
+      Or[r] = a.offsets[w0 + ic];
+    }
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int i = tid + r * kIcrcThreads;
@@ -614,8 +624,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
       offw[r] = kNoOff;
       lw[r] = 0;
       if (i < cnt) {
-        const uint32_t L = a.lens[w0 + i];
-        const uint64_t off = a.offsets[w0 + i];
+        const uint32_t L = Lr[r];
+        const uint64_t off = Or[r];
         if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
         lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
         if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
@@ -807,6 +817,16 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
     int keys[KR];
     uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
+    // every descriptor load of the thread first (clamped, unconditional: a
+    // guarded load makes the compiler wait for each in turn), then the keys
+    uint32_t Lr[KR];
+    uint64_t Or[KR];
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const int ic = min(tid + r * kIcrcThreads, cnt - 1);
+      Lr[r] = a.lens[w0 + ic];
+      Or[r] = a.offsets[w0 + ic];
+    }
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int i = tid + r * kIcrcThreads;
@@ -814,8 +834,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       offw[r] = kNoOff;
       lw[r] = 0;
       if (i < cnt) {
-        const uint32_t L = a.lens[w0 + i];
-        const uint64_t off = a.offsets[w0 + i];
+        const uint32_t L = Lr[r];
+        const uint64_t off = Or[r];
         if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
         lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
         if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
