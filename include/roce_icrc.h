@@ -83,7 +83,10 @@ void ricrc_ctx_destroy(ricrc_ctx* ctx);
 /* Lanes cooperating on one packet (1,2,4,...,64); 0 = automatic by length
  * (strided frames with stride <= 128 bytes, a multiple of 4, then use the
  * lane-per-packet kernel with LDS-staged loads; any non-zero setting forces
- * the lane-group kernels). */
+ * the lane-group kernels).  For ragged batches 8 selects the mixed-width
+ * kernel, which runs sorted claims of short frames (<= 600 B) with 4 lanes
+ * per packet and the rest with 8; it is also the automatic choice of the
+ * device-resident ragged calls. */
 int ricrc_ctx_set_lanes_per_packet(ricrc_ctx* ctx, int lanes);
 /* The hipStream_t the synchronous host-buffer calls run on. */
 void* ricrc_ctx_stream(ricrc_ctx* ctx);

@@ -629,6 +629,30 @@ def test_mixed_width_claims(engine, mtus, n):
     np.testing.assert_array_equal(ok.cpu().numpy().astype(bool), expect)
 
 
+@pytest.mark.parametrize("n", [37, 20_011, 600_001])
+def test_host_ragged_tiny_frames(engine, n):
+    """Host-buffer ragged batches whose mean frame is <= 128 B (ACK-sized
+    48-B frames with a few 4-KiB ones mixed in) run one lane per packet
+    (ragged_log2g): compute and verify against the C oracle, through the
+    pinned staging block (small calls) and the device scratch (large)."""
+    rng = np.random.default_rng(n)
+    mtus = (4,) * 63 + (4096,)
+    buf, offs, lens = synth.mixed_mtu_frames(n, mtus=mtus, seed=n)
+    assert lens.mean() <= 128 or n < 64
+    want, _ = oracle_batch(buf, offsets=offs, lens=lens)
+    got, st = engine.compute_batch(buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+    assert (st == 0).all()
+    trail = offs.astype(np.int64) + lens.astype(np.int64) - 4
+    buf[(trail[:, None] + np.arange(4)[None, :]).reshape(-1)] = want.view(np.uint8)
+    bad = rng.choice(n, max(1, n // 97), replace=False)
+    buf[offs[bad].astype(np.int64) + 40] ^= 0x01
+    ok, got2, _ = engine.verify_batch(buf, offs, lens)
+    expect = np.ones(n, bool)
+    expect[bad] = False
+    np.testing.assert_array_equal(ok, expect)
+
+
 def test_offsets_above_16_gib(engine):
     """Frames placed beyond 2^34 bytes into one 17-GiB device buffer.  The
     ragged kernel keeps sorted offsets as u32 dwords (< 16 GiB) and takes a
