@@ -251,7 +251,12 @@ __device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
   {
     const uint8_t* q = body_addr<G>(p, jhh, gl);
 #pragma unroll
-    for (int u = 0; u < U; ++u) b.cur[u] = u < first ? ldg128(q + 16 * G * u) : u32x4{0, 0, 0, 0};
+    for (int u = 0; u < U; ++u)
+#ifdef RICRC_FIRST_BLOCK_PLAIN  // experiment: the first body block cached as well
+      b.cur[u] = u < first ? *(const u32x4*)(q + 16 * G * u) : u32x4{0, 0, 0, 0};
+#else
+      b.cur[u] = u < first ? ldg128(q + 16 * G * u) : u32x4{0, 0, 0, 0};
+#endif
   }
   b.wl = load_chunk<G>(p, JL, gl);
   return b;

@@ -464,8 +464,13 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
         h.z = t == 2 ? icrc : h.z;
         h.w = t == 3 ? icrc : h.w;
       }
+#ifdef RICRC_SEG_WHOLE_LINES  // experiment: the last line written whole (zeros past the frame)
+      stg128<kSegStorePol>(s.dst + 16 * gl, hold0);
+      if (jl > 0) stg128<kSegStorePol>(s.dst + 4 * idxL, holdL);
+#else
       if (4 * gl < s.T) stg128<kSegStorePol>(s.dst + 16 * gl, hold0);
       if (jl > 0 && idxL < s.T) stg128<kSegStorePol>(s.dst + 4 * idxL, holdL);
+#endif
     }
     if (pkt < a.npkts && gl == 0) {
       a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;
