@@ -122,7 +122,12 @@ __device__ __forceinline__ Pkt describe(const uint8_t* frames, uint32_t pkt, boo
 // cached loads, not the body's non-temporal ones, so the neighbour's read of
 // the same line hits L2 instead of going to HBM again: cfg2 +2.7 % (6148 ->
 // 6317 GiB/s), cfg3 +2.5 % (5670 -> 5806), 3 of 3 A/B rounds.
-template <int G>
+// SHARED: a cached load (the head and last iterations, whose lines the
+// neighbouring frames share); else non-temporal.  Cached loads of the first
+// body block as well measured cfg2 -3 %, cfg3 -2 %; the second head
+// iteration non-temporal cfg2 -0.3 %, cfg3 -0.2 % (2 rounds), so it stays
+// cached.
+template <int G, bool SHARED = true>
 __device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
   constexpr int DPI = 4 * G;
   const int kb = DPI * j + 4 * gl - p.S;
@@ -131,7 +136,10 @@ __device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
 #ifdef RICRC_EDGE_NT  // diagnostic build only: edge chunks non-temporal like the body
     v = ldg128(p.ab + 16 * (G * j + gl));
 #else
-    v = *(const u32x4*)(p.ab + 16 * (G * j + gl));
+    if constexpr (SHARED)
+      v = *(const u32x4*)(p.ab + 16 * (G * j + gl));
+    else
+      v = ldg128(p.ab + 16 * (G * j + gl));
 #endif
   }
   return v;
@@ -324,7 +332,7 @@ __device__ __forceinline__ void finish_packet(const IcrcArgs& a, const Pkt& p, B
   Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   uint32_t h0 = 0, h2 = 0;
   for (int j = 0; j < jhh; ++j) {
-    u32x4 w = (j == 0) ? b.wh0 : (j == 1) ? b.wh1 : load_chunk<G>(p, j, gl);
+    u32x4 w = (j == 0) ? b.wh0 : (j == 1) ? b.wh1 : load_chunk<G, false>(p, j, gl);
     fix_chunk5(w, DPI * j + 4 * gl - p.S, kLut, h0, h2);
     fold(A, w, kk);
   }
