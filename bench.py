@@ -4,26 +4,37 @@
 One step = one launch of the HIP ICRC kernel over one batch of synthetic frames
 already resident in HBM.  Default workload (N=1): BASELINE config 2, 2^20 RC
 SEND_MIDDLE frames with 4 KiB payloads (4140-B wire frames, compute mode).
-With --gpus N (one process per GPU via torch.distributed.run) each rank owns its
-round-robin shard of 2^20 packets (BASELINE config 4 at N = 8: 2^23 packets in
-total); there is no data-path collective, only a gloo barrier and a max-reduce
-of the timing (weak scaling).  --workload cfg3 / cfg5 run the other BASELINE
-configurations (mixed-MTU verify, 64-B payloads) with the same contract.
+With --gpus N (one process per GPU via torch.distributed.run) the default
+workload is BASELINE config 4: ONE stream of 2^20 N frames (seed 0x1C2C0004,
+2^23 packets at N = 8), packet i on rank i mod N; there is no data-path
+collective, only a gloo barrier, a max-reduce of the timing (weak scaling) and
+a gather of every rank's parity result.  --workload cfg3 / cfg5 run the other
+BASELINE configurations (mixed-MTU verify, 64-B payloads) with the same
+contract.
+
+Every rank checks its own GPU words against the CPU restatement of
+BTH.compute_icrc on a seeded sample of >= 65536 of its packets (all of them
+when fewer) and the line fails (exit status 3) on any mismatch.
 
 Printed (rank 0): ONE JSON line with the driver's keys plus
   roofline      -- achieved algorithmic GB/s of the ICRC kernel (per-launch
                    bytes / mean launch time from HIP events on the launch
                    stream) against the 8.0 TB/s HBM peak, and the PMC-measured
                    HBM traffic per launch when profiles/pmc_traffic_<workload>.json holds
-                   it for this workload;
+                   it for this workload AND for this very build (the file
+                   records the sha256 of the libroceicrc.so it was measured
+                   on; another build gives traffic null and says why);
   cpu_baseline  -- the per-packet Python restatement of BTH.compute_icrc
                    (datenlord/roce-sim src/roce.py:192-223, zlib.crc32), timed
-                   on this host's cores over a bounded sample (rank 0, N=1).
+                   on this host's cores over a bounded sample (rank 0, N=1);
+  parity        -- per-rank sampled bit-exactness against that restatement.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -42,6 +53,10 @@ WORKLOADS = {
     # name: (payload bytes (0 = mixed MTU), packets per GPU, seed, description)
     "cfg2": (4096, 1 << 20, 0x1C2C0001,
              "4 KiB-MTU RC SEND_MIDDLE frames (4140 B), ICRC compute, stride 4140"),
+    # one global stream, packet i on rank i mod N, 2^20 per GPU
+    "cfg4": (4096, 1 << 20, 0x1C2C0004,
+             "4 KiB-MTU RC SEND_MIDDLE frames (4140 B) of ONE stream seeded 0x1C2C0004, packet i "
+             "on GPU i mod N, ICRC compute, stride 4140"),
     "cfg5": (64, 1 << 24, 0x1C2C0005,
              "64-B payload SEND_MIDDLE-shaped frames (108 B), ICRC compute, stride 108"),
     "cfg3": (0, 1 << 20, 0x1C2C0003,
@@ -62,7 +77,8 @@ def parse_args():
     # launches (profiles/, DESIGN.md "Measurement"); 100 timed launches ~ 70 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: cfg2 on one GPU, cfg4 (the 8-GPU config) with N > 1")
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -97,6 +113,33 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_share() -> tuple[int, dict]:
+    """Worker processes for the CPU baseline: every CPU this process may run
+    on (sched_getaffinity), capped by a cgroup CPU quota (cpu.max) and by the
+    host's declared per-job thread budget (OMP_NUM_THREADS: the GPU pool sets
+    it to the box's CPU share, 16 per GPU, and its rules forbid larger pools);
+    returns (procs, the counts it was derived from)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = None
+    try:
+        omp = int(os.environ["OMP_NUM_THREADS"])
+    except (KeyError, ValueError):
+        pass
+    procs = min(x for x in (aff, quota, omp) if x)
+    return max(1, procs), {"affinity_cpus": aff, "cgroup_cpus": quota, "omp_num_threads": omp,
+                           "host_cpus": os.cpu_count()}
+
+
 def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: np.ndarray):
     """Per-packet zlib restatement (oracle/, the CPU "port" baseline) on this host.
 
@@ -114,11 +157,7 @@ def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: 
     one = np.array([orc.icrc_of_frame_at(buf, int(offs[i]), int(lens[i])) for i in range(n1)],
                    np.uint32)
     t1 = time.perf_counter() - t0
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    procs = max(1, min(16, cores))
+    procs, share = cpu_share()
     global _CPU_JOB
     _CPU_JOB = (buf, offs, lens)
     step = (n + procs * 4 - 1) // (procs * 4)
@@ -138,12 +177,17 @@ def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: 
         "value": round(passes * c_all / tn / 2**30, 4),
         "unit": "GiB/s",
         "cores": procs,
+        "procs": procs,
+        **share,
         "kind": "port",
         "sample": (f"Python zlib.crc32 restatement of BTH.compute_icrc per packet over the same "
                    f"host frames: {passes} pass(es) over {n} packets on a {procs}-process fork "
-                   f"pool ({tn:.2f} s); "
+                   f"pool ({tn:.2f} s; {procs} = this job's CPU share, see cpu_share()); "
                    f"single core {n1} packets {c_one / t1 / 2**30:.3f} GiB/s"),
         "single_core_GiBps": round(c_one / t1 / 2**30, 4),
+        # an upper estimate for a pool over every CPU of the affinity mask
+        # (linear in the single-core rate; not measured)
+        "single_core_x_affinity_GiBps": round(c_one / t1 / 2**30 * share["affinity_cpus"], 2),
         "cpu_model": cpu_model(),
         "parity_mismatches_vs_gpu": mism,
     }
@@ -164,6 +208,7 @@ class Strided:
         self.torch, self.eng, self.n = torch, eng, n
         self.buf, self.stride, self.flen = synth.uniform_frames(
             n, payload, seed=seed if world == 1 else seed + rank, psn_start=rank, psn_step=world)
+        # (cfg2 / cfg5 at N > 1: one independent replica batch per rank)
         self.offs = np.arange(n, dtype=np.uint64) * self.stride
         self.lens = np.full(n, self.flen, np.uint32)
         self.covered = n * (self.flen - 4)
@@ -186,21 +231,44 @@ class Strided:
 
     def check(self):
         # self-consistency on the device (the bit-exact parity against the
-        # oracle is the cpu_baseline leg's and the test suite's): the words of
-        # the last step written into the trailers must all verify, and a frame
-        # with one payload bit flipped must not.  The frames are restored from
-        # the host copy by the host-inclusive leg that follows.
+        # oracle is the parity leg's, the cpu_baseline leg's and the test
+        # suite's): the words of the last step written into the trailers must
+        # all verify, and a frame with one payload bit flipped must not.  The
+        # touched bytes are restored afterwards, so the device frames are the
+        # host frames again whatever runs next.
         torch, n, S, L = self.torch, self.n, self.stride, self.flen
         rows = self.d_frames[:n * S].view(n, S)
+        saved = rows[:, L - 4:L].clone()
         rows[:, L - 4:L] = self.out.view(torch.uint8).view(n, 4)
         mid = n // 2
         rows[mid, L - 8] = rows[mid, L - 8] ^ 1  # last payload dword (covered, unmasked)
         ok = torch.zeros(n, dtype=torch.uint8, device=self.d_frames.device)
         self.eng.verify_strided_dev(self.d_frames, S, L, n, ok)
         okh = ok.cpu().numpy().astype(bool)
+        rows[mid, L - 8] = rows[mid, L - 8] ^ 1
+        rows[:, L - 4:L] = saved
         good = int(okh.sum())
         return {"words_verified": good, "frames": n, "flipped_frame_fails": bool(not okh[mid]),
                 "pass": bool(good == n - 1 and not okh[mid])}
+
+
+class Shard(Strided):
+    """cfg4: this rank's round-robin shard (packets i = rank mod world) of ONE
+    stream of n * world frames seeded 0x1C2C0004; the rank
+    generates only its own packets (synth.shard_frames)."""
+
+    def __init__(self, torch, eng, dev, payload, n, seed, rank, world):
+        from roce_icrc import synth
+        self.torch, self.eng = torch, eng
+        self.buf, self.stride, self.flen, self.gidx = synth.shard_frames(
+            n * world, rank, world, payload, seed=seed)
+        self.n = n = self.gidx.size
+        self.offs = np.arange(n, dtype=np.uint64) * self.stride
+        self.lens = np.full(n, self.flen, np.uint32)
+        self.covered = n * (self.flen - 4)
+        self.alg_bytes = n * self.flen
+        self.d_frames = torch.from_numpy(self.buf).to(dev)
+        self.out = torch.zeros(n, dtype=torch.int32, device=dev)
 
 
 class RaggedVerify:
@@ -289,11 +357,7 @@ def cpu_baseline_seg(mr: np.ndarray, rec: np.ndarray, pmtu: int, frames_ok):
 
     import segment_oracle as so
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    procs = max(1, min(16, cores))
+    procs, share = cpu_share()
     mv = memoryview(mr)
 
     def sample(nw):
@@ -323,6 +387,8 @@ def cpu_baseline_seg(mr: np.ndarray, rec: np.ndarray, pmtu: int, frames_ok):
         "value": round(cov / tn / 2**30, 4),
         "unit": "GiB/s",
         "cores": procs,
+        "procs": procs,
+        **share,
         "kind": "port",
         "sample": (f"Python restatement of process_send_req + IPv4/UDP/BTH serialisation + "
                    f"zlib ICRC per packet (oracle/segment_oracle.py): {nw} WRs = "
@@ -395,6 +461,67 @@ class Segment:
                 "pass": bool(nv == self.n and lens_ok)}
 
 
+PARITY_SAMPLE = 1 << 16  # packets per rank checked against the CPU restatement
+
+
+def parity_leg(W, gpu_icrc: np.ndarray, seed: int) -> dict:
+    """This rank's GPU ICRC words against the oracle's per-packet restatement
+    of BTH.compute_icrc (src/roce.py:192-223) on a seeded sample of its
+    packets (all of them when there are fewer than PARITY_SAMPLE); for
+    segmentation, the frames and words of the first WR against
+    segment_oracle.  Oracle use is confined to this checker."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    t0 = time.perf_counter()
+    if isinstance(W, Segment):
+        import segment_oracle as so
+        ok = W.frames_ok()
+        r = W.rec[0]
+        wr = so.SegWR(op=int(r["op"]), mr_offset=int(r["mr_offset"]), length=int(r["length"]),
+                      psn=int(r["psn"]), dqpn=int(r["dqpn"]), src_ip=int(r["src_ip"]),
+                      dst_ip=int(r["dst_ip"]), sport=int(r["sport"]), flags=int(r["flags"]),
+                      imm=int(r["imm"]))
+        want = so.segment(memoryview(W.mr), [wr], W.pmtu)
+        mism = sum(int(not ok(p, f)) for p, f in enumerate(want))
+        mism += sum(int(gpu_icrc[p]) != int.from_bytes(f[-4:], "little") for p, f in enumerate(want))
+        return {"sampled": len(want), "mismatches": mism, "what": "frames + ICRC words of WR 0",
+                "s": round(time.perf_counter() - t0, 2)}
+    import icrc_oracle as orc
+    n = gpu_icrc.size
+    k = min(n, PARITY_SAMPLE)
+    idx = (np.sort(np.random.default_rng(seed).choice(n, size=k, replace=False)) if k < n
+           else np.arange(n))
+    want = np.array([orc.icrc_of_frame_at(W.buf, int(W.offs[i]), int(W.lens[i])) for i in idx],
+                    np.uint32)
+    return {"sampled": int(k), "mismatches": int((want != gpu_icrc[idx]).sum()),
+            "what": "ICRC words of a seeded packet sample", "s": round(time.perf_counter() - t0, 2)}
+
+
+def lib_sha256() -> str:
+    from roce_icrc import engine as E
+    return hashlib.sha256(E.library_path().read_bytes()).hexdigest()
+
+
+def pmc_traffic(workload: str, n: int) -> tuple[int | None, str]:
+    """PMC HBM traffic per launch from profiles/pmc_traffic_<workload>.json,
+    only when that file was measured on THIS libroceicrc.so (sha256) and this
+    batch size; else (None, why)."""
+    pmc_file = PMC_DIR / f"pmc_traffic_{workload}.json"
+    if not pmc_file.exists():
+        return None, f"{pmc_file.name} absent"
+    try:
+        pmc = json.loads(pmc_file.read_text())
+    except (ValueError, OSError) as e:
+        return None, f"{pmc_file.name} unreadable ({e})"
+    if pmc.get("workload") != workload or pmc.get("packets") != n:
+        return None, f"{pmc_file.name} is for {pmc.get('workload')} x {pmc.get('packets')} packets"
+    sha = lib_sha256()
+    if pmc.get("lib_sha256") != sha:
+        return None, (f"{pmc_file.name} was measured on libroceicrc.so "
+                      f"{(pmc.get('lib_sha256') or 'unrecorded')[:12]}, this build is {sha[:12]}: "
+                      "not this build's traffic")
+    return pmc.get("traffic_bytes_per_launch"), f"{pmc_file.name}, same build (sha256 {sha[:12]})"
+
+
 CEIL_MIN_S = float(os.environ.get("ROCE_ICRC_CEIL_S", "0.08"))  # ceiling series length (s)
 
 
@@ -459,10 +586,12 @@ def main():
     from roce_icrc import IcrcEngine
 
     eng = IcrcEngine(local, lanes=args.lanes)
+    if args.workload is None:
+        args.workload = "cfg2" if world == 1 else "cfg4"
     payload, n_default, seed, desc = WORKLOADS[args.workload]
     n = args.packets or n_default
     dev = torch.device("cuda", local)
-    W = {"cfg3": RaggedVerify, "seg": Segment}.get(args.workload, Strided)(
+    W = {"cfg3": RaggedVerify, "seg": Segment, "cfg4": Shard}.get(args.workload, Strided)(
         torch, eng, dev, payload, n, seed, rank, world)
     n = W.n
     stream = torch.cuda.current_stream(dev)
@@ -514,6 +643,12 @@ def main():
     t_max = float(t[0])
     gpu_icrc = W.results()
     checks = W.check()
+    parity = parity_leg(W, gpu_icrc, seed + 101 * rank)
+    parity["rank"] = rank
+    parities = [parity]
+    if world > 1:
+        parities = [None] * world
+        dist.all_gather_object(parities, parity)
 
     # host-inclusive rate: pinned H2D of the frames + kernel + D2H of the results
     e2e = None
@@ -548,15 +683,7 @@ def main():
     if rank == 0:
         mean_k = float(np.mean(kern_s))
         achieved = W.alg_bytes / mean_k / 1e9
-        traffic = None
-        pmc_file = PMC_DIR / f"pmc_traffic_{args.workload}.json"
-        if pmc_file.exists():
-            try:
-                pmc = json.loads(pmc_file.read_text())
-                if pmc.get("workload") == args.workload and pmc.get("packets") == n:
-                    traffic = pmc.get("traffic_bytes_per_launch")
-            except (ValueError, OSError):
-                traffic = None
+        traffic, traffic_src = pmc_traffic(args.workload, n)
         value = world * W.covered * args.steps / t_max / 2**30
         line = {
             "metric": METRIC,
@@ -586,9 +713,17 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": W.alg_bytes,
             },
             "cpu_baseline": cpu,
+            "parity": {
+                "vs": "oracle/ CPU restatement of BTH.compute_icrc (zlib.crc32), per rank",
+                "sampled_per_rank": [p["sampled"] for p in parities],
+                "mismatches_per_rank": [p["mismatches"] for p in parities],
+                "what": parities[0]["what"],
+                "pass": all(p["mismatches"] == 0 for p in parities),
+            },
             "per_gpu_GiBps": round(value / world, 3),
             "kernel_ms_mean": round(mean_k * 1e3, 4),
             ceil_key: round(ceil_gbps, 1),
@@ -598,7 +733,8 @@ def main():
             line["checks"] = checks
         print(json.dumps(line), flush=True)
     failed = [k for k, bad in (("checks", checks and not checks.get("pass", True)),
-                                ("cpu parity", bool(cpu and cpu.get("parity_mismatches_vs_gpu"))))
+                                ("cpu parity", bool(cpu and cpu.get("parity_mismatches_vs_gpu"))),
+                                ("sampled parity", any(p["mismatches"] for p in parities)))
               if bad]
     if world > 1:
         dist.barrier()

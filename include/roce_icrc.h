@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define RICRC_ABI_VERSION 2
+#define RICRC_ABI_VERSION 3
 
 /* call-level return codes */
 #define RICRC_OK 0
@@ -147,6 +147,13 @@ int ricrc_verify_strided_dev(ricrc_ctx* ctx, const uint8_t* d_frames, uint64_t s
  *   TXLogic.process_send_req    src/roce_sq.py:1243   one ricrc_seg_wr of op SEND*
  *   TXLogic.process_write_req   src/roce_sq.py:1323   one ricrc_seg_wr of op RDMA_WRITE*
  *   ReadReqCtx.commit           src/roce_rq.py:388    one ricrc_seg_wr of op READ_RESPONSE
+ *   TXLogic.process_read_req    src/roce_sq.py:1413   op READ_REQUEST (BTH + RETH)
+ *   TXLogic.process_atomic_req  src/roce_sq.py:1441   op COMPARE_SWAP / FETCH_ADD (+ AtomicETH)
+ *   RXLogic.process_ack         src/roce_rq.py:767    op ACK (AETH ACK, value 31)
+ *   RXLogic.process_nak_rnr     src/roce_rq.py:778    op RNR_NAK (AETH RNR, value = imm)
+ *   RXLogic.process_nak_seq_err src/roce_rq.py:805    op NAK, imm 0 (AETH NAK, value 0)
+ *   RXLogic.process_nak_err     src/roce_rq.py:827    op NAK, imm 1 / 2 / 3 (or 31)
+ *   AtomicReqCtx.commit         src/roce_rq.py:490    op ATOMIC_ACK (AETH ACK 31 + AtomicAckETH)
  *   Util.compute_wr_pkt_num     src/roce_util.py:183  ricrc_segment_plan
  *   Util.add_padding_if_needed  src/roce_util.py:187  (in the kernel)
  *   IP()/UDP() wrap of send_ip_pkt / send_pkt         (in the kernel: IPv4 id 1, ttl 64,
@@ -164,6 +171,19 @@ int ricrc_verify_strided_dev(ricrc_ctx* ctx, const uint8_t* d_frames, uint64_t s
  * = SOLICITED on the last packet only (solicited only for SEND* and
  * RDMA_WRITE_WITH_IMM, as the reference), and its ICRC.
  *
+ * Header-only ops are one packet each and read no MR bytes (mr_offset and
+ * flags unused; `length` is RETH.dlen for READ_REQUEST and ignored otherwise):
+ *   READ_REQUEST        0x0C  ackreq 1, RETH(remote_va, rkey, length)
+ *   COMPARE_SWAP        0x13  ackreq 1, AtomicETH(remote_va, rkey, swap, comp)
+ *   FETCH_ADD           0x14  ackreq 1, AtomicETH(remote_va, rkey, swap, comp)
+ *   ACK                 0x11  AETH(code ACK, value 31 = CREDIT_CNT_INVALID, msn)
+ *   RNR_NAK             0x11  AETH(code RNR, value imm & 31 (min RNR timer), msn)
+ *   NAK                 0x11  AETH(code NAK, value imm & 31: 0 sequence error, 1
+ *                             invalid request, 2 remote access, 3 remote op, msn)
+ *   ATOMIC_ACK          0x12  AETH(ACK, 31, msn), AtomicAckETH(orig = swap)
+ * (PSN = psn, no solicited bit.)  A batch may mix every op: data and
+ * header-only packets of one call are built by ONE segmentation launch.
+ *
  * Output: packet p (WR order, packet order) is the wire frame at
  * frames + p * slot_bytes, lens[p] bytes long (0 with status
  * RICRC_PKT_SEG_BAD when its WR is invalid); slot bytes past the frame end, up
@@ -175,27 +195,38 @@ int ricrc_verify_strided_dev(ricrc_ctx* ctx, const uint8_t* d_frames, uint64_t s
 #define RICRC_SEG_RDMA_WRITE 3
 #define RICRC_SEG_RDMA_WRITE_WITH_IMM 4
 #define RICRC_SEG_READ_RESPONSE 5
+#define RICRC_SEG_READ_REQUEST 6
+#define RICRC_SEG_COMPARE_SWAP 7
+#define RICRC_SEG_FETCH_ADD 8
+#define RICRC_SEG_ACK 9
+#define RICRC_SEG_RNR_NAK 10
+#define RICRC_SEG_NAK 11
+#define RICRC_SEG_ATOMIC_ACK 12
+#define RICRC_SEG_NUM_OPS 13
 #define RICRC_SEG_SIGNALED 0x1  /* SEND_FLAGS.SIGNALED (src/roce_sq.py:1256)  */
 #define RICRC_SEG_SOLICITED 0x2 /* SEND_FLAGS.SOLICITED (src/roce_sq.py:1257) */
 #define RICRC_PKT_SEG_BAD 0x20  /* WR op unknown, MR range out of bounds, or packet not covered */
 
 typedef struct ricrc_seg_wr {
   uint64_t mr_offset; /* message start: byte offset into the MR buffer (any alignment) */
-  uint64_t remote_va; /* RETH.va (RDMA WRITE)                                         */
+  uint64_t remote_va; /* RETH.va (RDMA WRITE, READ_REQUEST), AtomicETH.va             */
+  uint64_t swap;      /* AtomicETH.swap; AtomicAckETH.orig (ATOMIC_ACK)               */
+  uint64_t comp;      /* AtomicETH.comp (compare value / FETCH_ADD addend)            */
   uint32_t length;    /* message bytes; 0 = one packet without payload                */
   uint32_t psn;       /* PSN of the first packet (24 bits)                            */
   uint32_t dqpn;      /* BTH.dqpn (24 bits)                                           */
   uint32_t src_ip;    /* IPv4 source as an integer (10.1.1.48 = 0x0A010130)           */
   uint32_t dst_ip;    /* IPv4 destination                                             */
-  uint32_t rkey;      /* RETH.rkey (RDMA WRITE)                                       */
-  uint32_t imm;       /* ImmDt.data (*_WITH_IMM) or IETH.rkey (SEND_WITH_INV)         */
-  uint32_t msn;       /* AETH.msn (READ_RESPONSE, 24 bits)                            */
+  uint32_t rkey;      /* RETH.rkey, AtomicETH.rkey                                    */
+  uint32_t imm;       /* ImmDt.data (*_WITH_IMM), IETH.rkey (SEND_WITH_INV), AETH
+                         value (RNR_NAK, NAK)                                         */
+  uint32_t msn;       /* AETH.msn (READ_RESPONSE, ACK, NAKs, ATOMIC_ACK; 24 bits)     */
   uint16_t sport;     /* UDP source port = the sender's QPN (src/roce_sq.py:1191)     */
   uint8_t op;         /* RICRC_SEG_*                                                  */
   uint8_t flags;      /* RICRC_SEG_SIGNALED | RICRC_SEG_SOLICITED                     */
   uint32_t first_pkt; /* index of the WR's first packet; set by ricrc_segment_plan    */
   uint32_t reserved[2];
-} ricrc_seg_wr; /* 64 bytes */
+} ricrc_seg_wr; /* 80 bytes */
 
 /* Host-only planning (no GPU): checks every WR's op, fills wrs[i].first_pkt
  * with the running packet count, returns the total packets and the slot size
@@ -216,7 +247,8 @@ int ricrc_segment(ricrc_ctx* ctx, const uint8_t* mr, size_t mr_bytes, const ricr
  * d_frames 256-byte aligned).  d_lens doubles as the packet -> WR map while
  * the call runs.  WRs are validated on the device (status RICRC_PKT_SEG_BAD,
  * length 0).  No byte outside [d_mr, d_mr + mr_bytes) is read, except that an
- * MR shorter than 16 bytes must be readable for 16. */
+ * MR shorter than 16 bytes must be readable for 16 when some packet carries
+ * payload (a batch of header-only ops and empty messages may pass d_mr NULL). */
 int ricrc_segment_dev(ricrc_ctx* ctx, const uint8_t* d_mr, uint64_t mr_bytes,
                       const ricrc_seg_wr* d_wrs, uint32_t nwr, uint32_t pmtu, uint32_t npkts,
                       uint8_t* d_frames, uint32_t slot_bytes, uint32_t* d_lens,

@@ -27,6 +27,19 @@ imported here because scapy is absent):
   serialisation, both through ``icrc_oracle.build_frame``.
 * PSN of packet k: ``cpsn + k``, a 24-bit BTH field (scapy masks it), i.e.
   ``(cpsn + k) mod 2^24``.
+* Header-only packets, one per WR, no payload:
+  ``TXLogic.process_read_req`` ``src/roce_sq.py:1413-1439`` -- BTH(
+  RDMA_READ_REQUEST, psn, dqpn, ackreq=True) / RETH(va, rkey, dlen=size);
+  ``TXLogic.process_atomic_req`` ``src/roce_sq.py:1441-1466`` -- BTH(
+  COMPARE_SWAP | FETCH_ADD, ackreq=True) / AtomicETH(va, rkey, comp, swap);
+  ``RXLogic.process_ack`` ``src/roce_rq.py:767-776`` -- BTH(ACKNOWLEDGE) /
+  AETH(code ACK, value CREDIT_CNT_INVALID, msn); ``process_nak_rnr``
+  ``:778-788`` -- AETH(code RNR, value = min_rnr_timer, msn);
+  ``process_nak_seq_err`` ``:805-814`` -- AETH(code NAK, value 0, msn);
+  ``process_nak_err`` ``:827-853`` -- AETH(code NAK, value 1 / 2 / 3, msn);
+  ``AtomicReqCtx.commit`` ``src/roce_rq.py:517-525`` -- BTH(
+  ATOMIC_ACKNOWLEDGE) / AETH(ACK, CREDIT_CNT_INVALID, msn) /
+  AtomicAckETH(orig).  The AETH value is a 5-bit field, the msn 24 bits.
 
 Parity status: **parity unpinned** for the segmentation rules (no reference
 test holds segmented frames; restated from the file:line ranges above).  The
@@ -45,6 +58,9 @@ import icrc_oracle as O  # noqa: E402
 
 # WR operations (include/roce_icrc.h RICRC_SEG_*)
 SEND, SEND_WITH_IMM, SEND_WITH_INV, RDMA_WRITE, RDMA_WRITE_WITH_IMM, READ_RESPONSE = range(6)
+READ_REQUEST, COMPARE_SWAP, FETCH_ADD, ACK, RNR_NAK, NAK, ATOMIC_ACK = range(6, 13)
+HEADER_ONLY = (READ_REQUEST, COMPARE_SWAP, FETCH_ADD, ACK, RNR_NAK, NAK, ATOMIC_ACK)
+AETH_ACK, AETH_RNR, AETH_NAK = 0, 1, 3  # AETH.code, src/roce.py:267
 SIGNALED, SOLICITED = 1, 2
 CREDIT_CNT_INVALID = 31  # src/roce_enum.py:8
 MAX_PSN = 1 << 24  # src/roce_enum.py:19
@@ -58,6 +74,8 @@ OP = dict(
     RDMA_READ_RESPONSE_FIRST=0x0D, RDMA_READ_RESPONSE_MIDDLE=0x0E,
     RDMA_READ_RESPONSE_LAST=0x0F, RDMA_READ_RESPONSE_ONLY=0x10,
     SEND_LAST_WITH_INVALIDATE=0x16, SEND_ONLY_WITH_INVALIDATE=0x17,
+    RDMA_READ_REQUEST=0x0C, ACKNOWLEDGE=0x11, ATOMIC_ACKNOWLEDGE=0x12, COMPARE_SWAP=0x13,
+    FETCH_ADD=0x14,
 )
 
 
@@ -78,11 +96,20 @@ class SegWR:
     remote_va: int = 0
     rkey: int = 0
     msn: int = 0
+    swap: int = 0  # AtomicETH.swap; AtomicAckETH.orig for ATOMIC_ACK
+    comp: int = 0  # AtomicETH.comp
 
 
 def wr_pkt_num(size: int, mtu: int) -> int:
     """Util.compute_wr_pkt_num, src/roce_util.py:183-185."""
     return math.ceil(size / mtu) if size > 0 else 1
+
+
+def packets_of(wr: SegWR, mtu: int) -> int:
+    """Packets one WR emits: compute_wr_pkt_num for the payload ops, 1 for the
+    header-only ones (a read request asks for its response packets but is one
+    packet itself, src/roce_sq.py:1413-1439)."""
+    return 1 if wr.op in HEADER_ONLY else wr_pkt_num(wr.length, mtu)
 
 
 def _ip(a: int) -> str:
@@ -139,6 +166,23 @@ def wr_packets(wr: SegWR, mtu: int):
                 opc, ext = OP["RDMA_WRITE_LAST"], b""
         bth = dict(opcode=opc, psn=psn(n - 1), dqpn=wr.dqpn, ackreq=int(sig), solicited=solicited)
         out.append((bth, ext, last_slice))
+    elif wr.op == READ_REQUEST:  # src/roce_sq.py:1421-1428
+        bth = dict(opcode=OP["RDMA_READ_REQUEST"], psn=psn(0), dqpn=wr.dqpn, ackreq=1)
+        out.append((bth, O.reth_bytes(wr.remote_va, wr.rkey, wr.length), None))
+    elif wr.op in (COMPARE_SWAP, FETCH_ADD):  # src/roce_sq.py:1444-1463
+        opc = OP["COMPARE_SWAP" if wr.op == COMPARE_SWAP else "FETCH_ADD"]
+        bth = dict(opcode=opc, psn=psn(0), dqpn=wr.dqpn, ackreq=1)
+        out.append((bth, O.atomic_eth_bytes(wr.remote_va, wr.rkey, wr.swap, wr.comp), None))
+    elif wr.op in (ACK, RNR_NAK, NAK):  # src/roce_rq.py:767-853
+        code = {ACK: AETH_ACK, RNR_NAK: AETH_RNR, NAK: AETH_NAK}[wr.op]
+        value = CREDIT_CNT_INVALID if wr.op == ACK else wr.imm & 0x1F
+        bth = dict(opcode=OP["ACKNOWLEDGE"], psn=psn(0), dqpn=wr.dqpn)
+        out.append((bth, O.aeth_bytes(code=code, value=value, msn=wr.msn & 0xFFFFFF), None))
+    elif wr.op == ATOMIC_ACK:  # src/roce_rq.py:517-525
+        bth = dict(opcode=OP["ATOMIC_ACKNOWLEDGE"], psn=psn(0), dqpn=wr.dqpn)
+        ext = O.aeth_bytes(code=AETH_ACK, value=CREDIT_CNT_INVALID, msn=wr.msn & 0xFFFFFF) + \
+            O.atomic_ack_eth_bytes(wr.swap)
+        out.append((bth, ext, None))
     elif wr.op == READ_RESPONSE:
         aeth = O.aeth_bytes(code=0, value=CREDIT_CNT_INVALID, msn=wr.msn)
         for k in range(n - 1):  # src/roce_rq.py:399-421

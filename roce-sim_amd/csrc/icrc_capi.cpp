@@ -25,9 +25,17 @@ struct ricrc_ctx {
   int lanes = 0;  // 0 = automatic
   hipStream_t stream = nullptr;
   uint32_t* d_tables = nullptr;
-  // tail-claim counters of the strided kernel (kClaimSlots x kMaxClaimBlocks)
+  // tail-claim counters of the strided kernel: one region of kClaimSlots x
+  // kMaxClaimBlocks counters per stream the context has launched on (up to
+  // kClaimStreams streams).  Launches on one stream run in order, so a slot
+  // is reused only after the launch 64 epochs earlier on the SAME stream has
+  // finished; two streams never share a region (see claim_region).
   unsigned long long* d_claims = nullptr;
-  uint32_t claim_epoch = 0;
+  struct ClaimRegion {
+    hipStream_t stream;
+    uint32_t epoch;
+  };
+  std::vector<ClaimRegion> claim_regions;
   // scratch for the host-buffer entry points
   uint8_t* d_frames = nullptr;
   size_t frames_cap = 0;
@@ -157,6 +165,23 @@ bool use_small(const ricrc_ctx* c, uint64_t stride, uint32_t len) {
          len >= 4;
 }
 
+// Claim counters for a strided launch on stream `s`: the stream's own region
+// and its next epoch, or nullptr (static ranges only, still correct) once
+// kClaimStreams distinct streams have a region.  A slot of a region is shared
+// only by launches 64 epochs apart on that one in-order stream, so a launch
+// never finds its counters overwritten by a concurrent launch on another
+// stream (which would silently drop its tail sets).
+unsigned long long* claim_region(ricrc_ctx* c, hipStream_t s, uint32_t* epoch) {
+  size_t r = 0;
+  while (r < c->claim_regions.size() && c->claim_regions[r].stream != s) ++r;
+  if (r == c->claim_regions.size()) {
+    if (r >= (size_t)ricrc::kClaimStreams) return nullptr;
+    c->claim_regions.push_back({s, 0u});
+  }
+  *epoch = ++c->claim_regions[r].epoch;  // (slot = epoch % kClaimSlots)
+  return c->d_claims + r * (size_t)ricrc::kClaimSlots * ricrc::kMaxClaimBlocks;
+}
+
 int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint32_t* lens,
            uint64_t stride, uint32_t len, uint32_t n, uint32_t* icrc, uint8_t* status, uint8_t* ok,
            bool ragged, bool verify, int log2g, hipStream_t s) {
@@ -175,10 +200,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0) {
     HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
   } else {
-    if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) {
-      a.claims = c->d_claims;
-      a.epoch = ++c->claim_epoch;  // (slot epoch % kClaimSlots of the counters)
-    }
+    if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
   }
   return RICRC_OK;
@@ -285,6 +307,9 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
 // starts at grid column 0 for up to 16 lanes per packet.
 uint32_t seg_slot_bytes(uint32_t pmtu) { return (60u + pmtu + 4u + 255u) & ~255u; }
 
+// Ops whose packets carry MR bytes (the rest are header-only, one packet).
+bool seg_has_payload(uint32_t op) { return op <= RICRC_SEG_READ_RESPONSE; }
+
 bool valid_pmtu(uint32_t pmtu) {
   return pmtu == 256 || pmtu == 512 || pmtu == 1024 || pmtu == 2048 || pmtu == 4096;
 }
@@ -382,7 +407,8 @@ int ricrc_ctx_create(int device, ricrc_ctx** out) {
   ricrc::build_table_image(img.data());
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->d_tables, img.size() * sizeof(uint32_t));
-  const size_t claim_bytes = sizeof(unsigned long long) * ricrc::kClaimSlots * ricrc::kMaxClaimBlocks;
+  const size_t claim_bytes = sizeof(unsigned long long) * ricrc::kClaimStreams *
+                             ricrc::kClaimSlots * ricrc::kMaxClaimBlocks;
   if (e == hipSuccess) e = hipMalloc(&c->d_claims, claim_bytes);
   if (e == hipSuccess) e = hipMemset(c->d_claims, 0, claim_bytes);
   if (e == hipSuccess)
@@ -595,10 +621,13 @@ int ricrc_segment_plan(ricrc_seg_wr* wrs, uint32_t nwr, uint32_t pmtu, uint32_t*
   if ((nwr && !wrs) || !npkts_out || !valid_pmtu(pmtu)) return RICRC_EINVAL;
   uint64_t total = 0;
   for (uint32_t i = 0; i < nwr; ++i) {
-    if (wrs[i].op > RICRC_SEG_READ_RESPONSE) return RICRC_EINVAL;
+    if (wrs[i].op >= RICRC_SEG_NUM_OPS) return RICRC_EINVAL;
     wrs[i].first_pkt = (uint32_t)total;
-    // Util.compute_wr_pkt_num (src/roce_util.py:183-185)
-    total += wrs[i].length ? ((uint64_t)wrs[i].length + pmtu - 1) / pmtu : 1;
+    // Util.compute_wr_pkt_num (src/roce_util.py:183-185); header-only ops
+    // (read request, atomics, ACK/NAK, atomic ack) are one packet each
+    total += !seg_has_payload(wrs[i].op) ? 1
+             : wrs[i].length              ? ((uint64_t)wrs[i].length + pmtu - 1) / pmtu
+                                          : 1;
     if (total > 0xFFFFFFFFull) return RICRC_EINVAL;
   }
   *npkts_out = (uint32_t)total;
@@ -616,8 +645,9 @@ int ricrc_segment(ricrc_ctx* c, const uint8_t* mr, size_t mr_bytes, const ricrc_
   int rc = ricrc_segment_plan(plan.data(), nwr, pmtu, &npkts, &slot);
   if (rc) return rc;
   for (uint32_t i = 0; i < nwr; ++i)
-    if (plan[i].first_pkt != wrs[i].first_pkt || wrs[i].mr_offset > mr_bytes ||
-        wrs[i].length > mr_bytes - wrs[i].mr_offset)
+    if (plan[i].first_pkt != wrs[i].first_pkt ||
+        (seg_has_payload(wrs[i].op) &&
+         (wrs[i].mr_offset > mr_bytes || wrs[i].length > mr_bytes - wrs[i].mr_offset)))
       return RICRC_EINVAL;
   if (npkts == 0) return RICRC_OK;
   if (!frames || !lens || frames_bytes < (size_t)npkts * slot) return RICRC_EINVAL;

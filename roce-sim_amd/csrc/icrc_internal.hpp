@@ -31,8 +31,10 @@ struct IcrcArgs {
   uint32_t epoch;
 };
 
-// Claim counters: kClaimSlots launches of one context may be in flight at
+// Claim counters: per stream (up to kClaimStreams streams per context; later
+// streams run without tail claims), kClaimSlots launches may be in flight at
 // once (slot = epoch % kClaimSlots), each with one counter per workgroup.
+constexpr int kClaimStreams = 16;
 constexpr int kClaimSlots = 64;
 constexpr int kMaxClaimBlocks = 1024;
 

@@ -1195,13 +1195,21 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     uint32_t in_ring = 0;
     auto flush = [&]() {
       const uint32_t words = min(in_ring * nw, bs_end - ring_base / 64u) * 64u;
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring words are written
+      // lgkmcnt(0): this wave's ring words are written.  The compiler-level
+      // memory clobbers pin the ring's LDS accesses on their side of the
+      // barrier (the barrier intrinsic alone is not a memory operation at IR
+      // level); they emit no wait, so the prefetched global loads stay in flight.
+      __asm__ __volatile__("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_s_barrier();
+      __asm__ __volatile__("" ::: "memory");
       const auto dst = out_rsrc(a.icrc_out + ring_base, 4u * words);
       for (uint32_t i = (uint32_t)tid; i < words / 4u; i += blockDim.x)
         out_store128<kSmallOutPol>(*(const lds_u32x4*)(uintptr_t)small_ring_quad(ring, i), dst, 16u * i);
+      __asm__ __volatile__("" ::: "memory");
       __builtin_amdgcn_s_waitcnt(0xC07F);  // the ring is read before anyone writes it again
       __builtin_amdgcn_s_barrier();
+      __asm__ __volatile__("" ::: "memory");
       ring_base += in_ring * nw * 64u;
       in_ring = 0;
     };

@@ -4,7 +4,10 @@
 // roce-sim's requester and responder emit for a batch of work requests:
 // TXLogic.process_send_req (src/roce_sq.py:1243-1321), process_write_req
 // (src/roce_sq.py:1323-1411) and ReadReqCtx.commit (src/roce_rq.py:388-438),
-// each packet wrapped in IPv4/UDP as send_ip_pkt / send_pkt do
+// and the header-only packets: process_read_req / process_atomic_req
+// (src/roce_sq.py:1413-1466), process_ack / process_nak_* (src/roce_rq.py:
+// 767-854) and the atomic acknowledge of AtomicReqCtx.commit
+// (src/roce_rq.py:490-525); each packet wrapped in IPv4/UDP as send_ip_pkt / send_pkt do
 // (src/roce_sq.py:1186-1197, src/roce_rq.py:705-731), padded as
 // Util.add_padding_if_needed (src/roce_util.py:187-199), with its IPv4 header
 // checksum, its ICRC (BTH.compute_icrc, src/roce.py:192-223) and its UDP
@@ -64,6 +67,8 @@ constexpr int kSegWaves = kSegThreads / 64;
 constexpr int kSegStorePol = RICRC_SEG_STORE_POL;
 constexpr uint32_t kRocePort = 4791;   // src/roce_enum.py ROCE_PORT
 constexpr uint32_t kAckValue = 31;     // CREDIT_CNT_INVALID, src/roce_enum.py:8
+// AETH.code (src/roce.py:267): ACK 0, RNR 1, NAK 3
+constexpr uint32_t kAethAck = 0, kAethRnr = 1, kAethNak = 3;
 constexpr uint32_t kPktSegBad = 0x20;  // RICRC_PKT_SEG_BAD
 
 __device__ __forceinline__ uint32_t wr_pkt_num(uint32_t len, uint32_t pmtu) {
@@ -76,12 +81,13 @@ struct Seg {
   const uint8_t* src;  // payload start in the MR
   uint8_t* dst;        // slot start
   uint32_t plen;       // payload bytes
+  const uint8_t* hi;   // highest start of a 16-byte payload read (see describe_seg)
   int hd;              // header dwords: IPv4 5 + UDP 2 + BTH 3 + extension headers
   int T;               // frame dwords incl. the ICRC slot
   int F;               // dwords fully defined without masking: hd + plen / 4
   // header dwords (big-endian values) except the checksums
   uint32_t h0, h3, h4, h5, h6, h7, h8, h9;
-  uint32_t e[5];       // extension header dwords
+  uint32_t e[7];       // extension header dwords (AtomicETH is the longest, 7)
   uint32_t ipcs;       // IPv4 header checksum
   bool live;
 };
@@ -95,18 +101,23 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s) {
 // The packet of index `pkt`: its WR, opcode, extension headers and geometry
 // (the rules of src/roce_sq.py:1243-1411 and src/roce_rq.py:388-438).
 __device__ __forceinline__ Seg describe_seg(const SegArgs& a, uint32_t pkt, bool inrange,
-                                            uint32_t& status) {
+                                            uint32_t& status, const uint8_t* mr_hi) {
   Seg s;
   status = 0;
   s.live = false;
-  s.src = a.mr;
   s.dst = a.frames + (uint64_t)pkt * a.slot;
+  // A packet without payload reads no MR byte: its (unconditional, masked)
+  // payload loads are clamped to the first 16 bytes of its own slot (of the
+  // frame buffer's first slot for a lane past the batch).
+  s.src = inrange ? s.dst : a.frames;
+  s.hi = s.src;
   s.plen = 0;
   s.hd = 10;
   s.T = 0;
   s.F = 0;
   s.h0 = s.h3 = s.h4 = s.h5 = s.h6 = s.h7 = s.h8 = s.h9 = 0;
-  s.e[0] = s.e[1] = s.e[2] = s.e[3] = s.e[4] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) s.e[i] = 0;
   s.ipcs = 0;
   if (!inrange) return s;
   const uint32_t w = a.lens[pkt];
@@ -115,10 +126,11 @@ __device__ __forceinline__ Seg describe_seg(const SegArgs& a, uint32_t pkt, bool
   const ricrc_seg_wr& wr = a.wrs[w];
   const uint64_t mo = wr.mr_offset;
   const uint32_t len = wr.length, op = wr.op;
-  const uint32_t n = wr_pkt_num(len, a.pmtu);
+  const bool data = op <= RICRC_SEG_READ_RESPONSE;  // packets carrying MR bytes
+  const uint32_t n = data ? wr_pkt_num(len, a.pmtu) : 1u;
   const uint32_t k = pkt - wr.first_pkt;
-  if (pkt < wr.first_pkt || k >= n || op > RICRC_SEG_READ_RESPONSE || mo > a.mr_bytes ||
-      len > a.mr_bytes - mo)
+  if (pkt < wr.first_pkt || k >= n || op >= RICRC_SEG_NUM_OPS ||
+      (data && (mo > a.mr_bytes || len > a.mr_bytes - mo)))
     return s;
   status = 0;
   s.live = true;
@@ -127,14 +139,52 @@ __device__ __forceinline__ Seg describe_seg(const SegArgs& a, uint32_t pkt, bool
   const bool sol = (wr.flags & RICRC_SEG_SOLICITED) != 0;
   // payload: full PMTU slices, the remainder on the last packet (none if len == 0)
   const uint32_t off = k * a.pmtu;
-  s.plen = last ? len - off : a.pmtu;
-  s.src = a.mr + mo + off;
+  if (data) {
+    s.plen = last ? len - off : a.pmtu;
+    if (s.plen) {
+      s.src = a.mr + mo + off;
+      s.hi = mr_hi;
+    }
+  }
 
-  uint32_t opc, ext = 0;  // ext: 0 none, 1 one dword (ImmDt/IETH/AETH), 4 RETH, 5 RETHImmDt
+  // ext: 0 none, 1 one dword (ImmDt/IETH/AETH), 3 AETH + AtomicAckETH,
+  // 4 RETH, 5 RETHImmDt, 7 AtomicETH
+  uint32_t opc, ext = 0;
   uint32_t e0 = 0;
   bool ack = false, se = false;
   const uint32_t va_hi = (uint32_t)(wr.remote_va >> 32), va_lo = (uint32_t)wr.remote_va;
-  if (op <= RICRC_SEG_SEND_WITH_INV) {
+  if (!data) {
+    const uint32_t msn = wr.msn & 0xFFFFFFu;
+    if (op == RICRC_SEG_READ_REQUEST) {  // src/roce_sq.py:1421-1428
+      opc = 0x0Cu;
+      ext = 4;  // RETH(va, rkey, dlen = length) below
+      ack = true;
+    } else if (op <= RICRC_SEG_FETCH_ADD) {  // src/roce_sq.py:1444-1463
+      opc = op == RICRC_SEG_COMPARE_SWAP ? 0x13u : 0x14u;
+      ext = 7;
+      ack = true;
+      s.e[0] = va_hi;
+      s.e[1] = va_lo;
+      s.e[2] = wr.rkey;
+      s.e[3] = (uint32_t)(wr.swap >> 32);
+      s.e[4] = (uint32_t)wr.swap;
+      s.e[5] = (uint32_t)(wr.comp >> 32);
+      s.e[6] = (uint32_t)wr.comp;
+    } else if (op == RICRC_SEG_ATOMIC_ACK) {  // src/roce_rq.py:517-524
+      opc = 0x12u;
+      ext = 3;
+      s.e[0] = (kAckValue << 24) | msn;
+      s.e[1] = (uint32_t)(wr.swap >> 32);  // AtomicAckETH.orig
+      s.e[2] = (uint32_t)wr.swap;
+    } else {  // ACKNOWLEDGE: ACK / RNR NAK / NAK, src/roce_rq.py:767-853
+      opc = 0x11u;
+      ext = 1;
+      const uint32_t code = op == RICRC_SEG_ACK ? kAethAck : op == RICRC_SEG_RNR_NAK ? kAethRnr
+                                                                                     : kAethNak;
+      const uint32_t value = op == RICRC_SEG_ACK ? kAckValue : (wr.imm & 31u);
+      e0 = (((code << 5) | value) << 24) | msn;
+    }
+  } else if (op <= RICRC_SEG_SEND_WITH_INV) {
     if (!last) {
       opc = first ? 0x00u : 0x01u;  // SEND_FIRST / SEND_MIDDLE
     } else {
@@ -173,13 +223,13 @@ __device__ __forceinline__ Seg describe_seg(const SegArgs& a, uint32_t pkt, bool
       e0 = (kAckValue << 24) | (wr.msn & 0xFFFFFFu);  // rsvd 0, code ACK 0, value 31, msn
     }
   }
-  if (ext >= 4) {
+  if (ext == 4 || ext == 5) {
     s.e[0] = va_hi;
     s.e[1] = va_lo;
     s.e[2] = wr.rkey;
-    s.e[3] = len;  // RETH.dlen = message length
+    s.e[3] = len;  // RETH.dlen = message length (READ_REQUEST: the read size)
     s.e[4] = wr.imm;
-  } else {
+  } else if (ext == 1) {
     s.e[0] = e0;
   }
   s.hd = 10 + (int)ext;
@@ -209,17 +259,17 @@ __device__ __forceinline__ Seg describe_seg(const SegArgs& a, uint32_t pkt, bool
 template <int t>
 __device__ __forceinline__ uint32_t header_dword(const Seg& s, int c) {
   constexpr uint32_t kId = 0x00010000u;  // id 1, flags/frag 0
-  uint32_t v0, v1, v2, v3;
+  uint32_t v0, v1, v2, v3, v4;
   if constexpr (t == 0) {
-    v0 = s.h0; v1 = s.h4; v2 = s.h8; v3 = s.e[2];
+    v0 = s.h0; v1 = s.h4; v2 = s.h8; v3 = s.e[2]; v4 = s.e[6];
   } else if constexpr (t == 1) {
-    v0 = kId; v1 = s.h5; v2 = s.h9; v3 = s.e[3];
+    v0 = kId; v1 = s.h5; v2 = s.h9; v3 = s.e[3]; v4 = 0u;
   } else if constexpr (t == 2) {
-    v0 = 0x40110000u | s.ipcs; v1 = s.h6; v2 = s.e[0]; v3 = s.e[4];  // ttl 64, proto 17
+    v0 = 0x40110000u | s.ipcs; v1 = s.h6; v2 = s.e[0]; v3 = s.e[4]; v4 = 0u;  // ttl 64, proto 17
   } else {
-    v0 = s.h3; v1 = s.h7; v2 = s.e[1]; v3 = 0u;
+    v0 = s.h3; v1 = s.h7; v2 = s.e[1]; v3 = s.e[5]; v4 = 0u;
   }
-  const uint32_t v = c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3;
+  const uint32_t v = c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : c == 3 ? v3 : v4;
   return __builtin_bswap32(v);
 }
 
@@ -305,7 +355,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
   for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kSegWaves) {
     const uint32_t pkt = set * PPW + grp;
     uint32_t status;
-    const Seg s = describe_seg(a, pkt, pkt < a.npkts, status);
+    const Seg s = describe_seg(a, pkt, pkt < a.npkts, status, mr_hi);
     // CRC geometry (frame at grid column 0): n covered dwords, J iterations,
     // r valid columns in the last one
     const int n = s.live ? s.T - 1 : 1;
@@ -320,10 +370,11 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
     // of a block >= 1 reads the 16 payload bytes at dword DPI j + 4 gl - hd
     // from one base pointer (immediate offsets); block 0 clamps header lanes
     // to dword 0.  Reads run up to one block past the frame (into the next
-    // packet's bytes); a wave that could read past the MR end takes the
+    // packet's bytes); a wave that could read past the MR end, or holds a
+    // packet without payload (whose loads stay in its own slot), takes the
     // clamped-and-shifted form of every load instead.
     const int far = max(DPI * (max(nblk, 2) * U - 1) + 4 * gl - s.hd, 0);
-    const bool guard = s.src + 4 * far + 16 > mr_end;
+    const bool guard = s.hi != mr_hi || s.src + 4 * far + 16 > mr_end;
 
     Col A = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     uint64_t acc = 0;
@@ -399,7 +450,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int m = max(DPI * min(bc * U + u, max(Jw - 1, 0)) + 4 * gl - s.hd, 0);
-            v[u] = load_payload_clamped(s.src + 4 * m, mr_hi);
+            v[u] = load_payload_clamped(s.src + 4 * m, s.hi);
           }
         } else {
           // iterations past the packet's last one re-read that one (no HBM
@@ -415,7 +466,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
       for (int u = 0; u < U; ++u) {
         const int m = max(DPI * u + 4 * gl - s.hd, 0);
         if constexpr (GUARD)
-          Y[u] = load_payload_clamped(s.src + 4 * m, mr_hi);
+          Y[u] = load_payload_clamped(s.src + 4 * m, s.hi);
         else
           Y[u] = ldmr(s.src + 4 * m);
       }
@@ -484,7 +535,9 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
 __global__ void __launch_bounds__(256) seg_map_kernel(SegArgs a) {
   for (uint32_t w = blockIdx.x; w < a.nwr; w += gridDim.x) {
     const uint32_t fp = a.wrs[w].first_pkt;
-    const uint32_t cnt = wr_pkt_num(a.wrs[w].length, a.pmtu);
+    // (header-only ops are one packet whatever their length field)
+    const uint32_t cnt =
+        a.wrs[w].op <= RICRC_SEG_READ_RESPONSE ? wr_pkt_num(a.wrs[w].length, a.pmtu) : 1u;
     for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
       const uint64_t p = (uint64_t)fp + k;
       if (p < a.npkts) a.lens[p] = w;

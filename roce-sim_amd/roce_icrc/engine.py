@@ -35,20 +35,24 @@ PKT_SEG_BAD = 0x20
 # segmentation work-request ops and flags (RICRC_SEG_*)
 SEG_SEND, SEG_SEND_WITH_IMM, SEG_SEND_WITH_INV = 0, 1, 2
 SEG_RDMA_WRITE, SEG_RDMA_WRITE_WITH_IMM, SEG_READ_RESPONSE = 3, 4, 5
+# header-only ops (one packet each, no MR bytes)
+SEG_READ_REQUEST, SEG_COMPARE_SWAP, SEG_FETCH_ADD = 6, 7, 8
+SEG_ACK, SEG_RNR_NAK, SEG_NAK, SEG_ATOMIC_ACK = 9, 10, 11, 12
+SEG_NUM_OPS = 13
 SEG_SIGNALED, SEG_SOLICITED = 0x1, 0x2
 
 # fault kinds (RICRC_FAULT_*)
 FAULT_ICRC, FAULT_PAYLOAD, FAULT_MASKED = 0x1, 0x2, 0x4
 
-# struct ricrc_seg_wr (include/roce_icrc.h), 64 bytes, as a numpy record so
+# struct ricrc_seg_wr (include/roce_icrc.h), 80 bytes, as a numpy record so
 # large WR batches are built vectorised
 SEG_WR_DTYPE = np.dtype([
-    ("mr_offset", "<u8"), ("remote_va", "<u8"), ("length", "<u4"), ("psn", "<u4"),
-    ("dqpn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("rkey", "<u4"), ("imm", "<u4"),
-    ("msn", "<u4"), ("sport", "<u2"), ("op", "u1"), ("flags", "u1"), ("first_pkt", "<u4"),
-    ("reserved", "<u4", (2,)),
+    ("mr_offset", "<u8"), ("remote_va", "<u8"), ("swap", "<u8"), ("comp", "<u8"),
+    ("length", "<u4"), ("psn", "<u4"), ("dqpn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"),
+    ("rkey", "<u4"), ("imm", "<u4"), ("msn", "<u4"), ("sport", "<u2"), ("op", "u1"),
+    ("flags", "u1"), ("first_pkt", "<u4"), ("reserved", "<u4", (2,)),
 ])
-assert SEG_WR_DTYPE.itemsize == 64
+assert SEG_WR_DTYPE.itemsize == 80
 
 
 class IcrcUnavailable(RuntimeError):
@@ -347,8 +351,12 @@ class IcrcEngine:
     def segment(self, mr, wrs: np.ndarray, pmtu: int):
         """Build every frame of a WR batch on the GPU (process_send_req /
         process_write_req / ReadReqCtx.commit, src/roce_sq.py:1243-1411,
-        src/roce_rq.py:388-438).  Plans ``wrs`` in place.  Returns
-        (frames [npkts, slot] uint8, lens, icrc, status)."""
+        src/roce_rq.py:388-438; header-only ops: process_read_req /
+        process_atomic_req src/roce_sq.py:1413-1466, process_ack /
+        process_nak_* src/roce_rq.py:767-854, the atomic acknowledge of
+        AtomicReqCtx.commit src/roce_rq.py:490-525), all in one launch.
+        Plans ``wrs`` in place.  Returns (frames [npkts, slot] uint8, lens,
+        icrc, status)."""
         m = _u8(mr)
         npkts, slot = segment_plan(wrs, pmtu)
         frames = np.zeros((npkts, slot), np.uint8)

@@ -91,6 +91,49 @@ def uniform_frames(n: int, payload_len: int = 4096, opcode: int = 0x01, seed: in
     return buf, frame_len, frame_len
 
 
+def shard_frames(n_total: int, rank: int, world: int, payload_len: int = 4096,
+                 opcode: int = 0x01, seed: int = SEED_CFG4,
+                 chunk: int = 1 << 14) -> tuple[np.ndarray, int, int, np.ndarray]:
+    """cfg4: ONE global stream of n_total frames built
+    like cfg2 from `seed`, packet i going to rank i mod world; returns this
+    rank's shard (packets rank, rank + world, ... in order) as (buffer,
+    stride, frame_len, global packet indices).
+
+    The global stream is the one ``uniform_frames(n_total, payload_len,
+    seed=seed)`` builds (payload words of packet i = 64-bit outputs
+    [i W, (i + 1) W) of PCG64(seed), W = payload_len / 8, each shifted right
+    by one bit as ``Generator.integers(0, 2**63 - 1)`` returns them; PSN = i
+    mod 2^24), so a rank generates only its own packets: the generator jumps
+    over the other ranks' words with ``PCG64.advance``.  At world = 1 the
+    shard is the whole uniform_frames batch, byte for byte."""
+    assert payload_len % 8 == 0 and 0 <= rank < world
+    idx = np.arange(rank, n_total, world, dtype=np.int64)
+    n = idx.size
+    frame_len = HDR + payload_len + ICRC
+    buf = np.empty(n * frame_len, dtype=np.uint8)
+    rows = buf.reshape(n, frame_len)
+    tmpl = header_template(payload_len, opcode)
+    W = payload_len // 8
+    bg = np.random.PCG64(seed)
+    if n:
+        bg.advance(int(idx[0]) * W)
+    skip = (world - 1) * W
+    words = np.empty((min(chunk, max(n, 1)), W), dtype=np.uint64)
+    one = np.uint64(1)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        for k in range(e - s):
+            words[k] = bg.random_raw(W)
+            if skip:
+                bg.advance(skip)
+        r = rows[s:e]
+        r[:, :HDR] = tmpl
+        _write_psn(r, idx[s:e])
+        r[:, HDR:HDR + payload_len] = (words[:e - s] >> one).view(np.uint8)
+        r[:, HDR + payload_len:] = 0
+    return buf, frame_len, frame_len, idx
+
+
 def mixed_mtu_frames(n: int, mtus=MTUS, opcode: int = 0x07, seed: int = SEED_CFG3,
                      chunk: int = 1 << 16) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
     """cfg3: n frames, payload = MTU drawn uniformly from `mtus`, packed

@@ -14,6 +14,7 @@ usage: python scripts/pmc_traffic.py --fetch DIR --write DIR --workload cfg2 \
 """
 import argparse
 import csv
+import hashlib
 import json
 from collections import defaultdict
 from pathlib import Path
@@ -55,6 +56,13 @@ def main():
     ap.add_argument("--ceiling", default="stream_read_kernel")
     ap.add_argument("--ceiling-read-bytes", type=int, default=0)
     ap.add_argument("--alg-bytes", type=int, default=0)
+    ap.add_argument("--lib", default=str(Path(__file__).resolve().parent.parent / "roce-sim_amd" /
+                                         "roce_icrc" / "libroceicrc.so"),
+                    help="the library the passes ran (its sha256 binds the figure to the build)")
+    ap.add_argument("--calibration", type=float, default=0.0,
+                    help="FETCH_SIZE factor measured on this workload's own access pattern "
+                         "(scripts/fetch_calib.py); default: the STREAM kernel of the same run")
+    ap.add_argument("--calibration-source", default="")
     a = ap.parse_args()
     fr = read_counters(a.fetch)
     wr = read_counters(a.write)
@@ -64,7 +72,9 @@ def main():
     # bench.py's ceiling kernel reads the whole frame buffer (ICRC) or the MR (seg)
     sr_bytes = a.ceiling_read_bytes or (n * flen) // 16 * 16
     fetch_sr = mean(fr[k_sr]["FETCH_SIZE"]) * 1024
-    calib = sr_bytes / fetch_sr
+    calib = a.calibration or sr_bytes / fetch_sr
+    calib_src = (a.calibration_source or "given") if a.calibration else \
+        f"{a.ceiling} in the same run: known bytes read / FETCH_SIZE"
     fetch_icrc_raw = mean(fr[k_icrc]["FETCH_SIZE"]) * 1024
     write_icrc = mean(wr[pick(wr, a.kernel)]["WRITE_SIZE"]) * 1024
     fetch_icrc = fetch_icrc_raw * calib
@@ -75,12 +85,14 @@ def main():
         "kernel": k_icrc,
         "fetch_size_raw_bytes": round(fetch_icrc_raw),
         "fetch_calibration": round(calib, 4),
-        "fetch_calibration_source": f"{a.ceiling} in the same run: known bytes read / FETCH_SIZE",
+        "fetch_calibration_source": calib_src,
+        "stream_kernel_calibration": round(sr_bytes / fetch_sr, 4),
         "fetch_bytes": round(fetch_icrc),
         "write_bytes": round(write_icrc),
         "traffic_bytes_per_launch": round(fetch_icrc + write_icrc),
         "alg_bytes_per_launch": alg,
         "traffic_over_alg": round((fetch_icrc + write_icrc) / alg, 4),
+        "lib_sha256": hashlib.sha256(Path(a.lib).read_bytes()).hexdigest(),
         "dispatches": {"fetch_pass": len(fr[k_icrc]["FETCH_SIZE"]),
                        "write_pass": len(wr[pick(wr, a.kernel)]["WRITE_SIZE"])},
     }

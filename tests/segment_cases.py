@@ -26,6 +26,8 @@ def to_records(wrs: list[SO.SegWR]) -> np.ndarray:
         rec[i]["remote_va"] = w.remote_va
         rec[i]["rkey"] = w.rkey
         rec[i]["msn"] = w.msn
+        rec[i]["swap"] = w.swap
+        rec[i]["comp"] = w.comp
     return rec
 
 
@@ -38,8 +40,9 @@ def lengths_for(pmtu: int) -> list[int]:
 def all_ops_cases(pmtu: int, mr_size: int, seed: int = 0) -> list[SO.SegWR]:
     rng = np.random.default_rng(seed)
     wrs = []
-    for op in range(6):
-        for length in lengths_for(pmtu):
+    for op in range(SO.ATOMIC_ACK + 1):
+        # header-only ops: lengths only reach RETH.dlen (READ_REQUEST)
+        for length in lengths_for(pmtu) if op < SO.READ_REQUEST else (0, 5, 3 * pmtu + 2):
             for flags in (0, SO.SIGNALED | SO.SOLICITED):
                 off = int(rng.integers(0, mr_size - length + 1))
                 wrs.append(SO.SegWR(
@@ -48,5 +51,6 @@ def all_ops_cases(pmtu: int, mr_size: int, seed: int = 0) -> list[SO.SegWR]:
                     src_ip=SRC_IP, dst_ip=DST_IP, sport=int(rng.integers(0, 1 << 16)),
                     flags=flags, imm=int(rng.integers(0, 1 << 32)),
                     remote_va=int(rng.integers(0, 1 << 63)), rkey=int(rng.integers(0, 1 << 32)),
-                    msn=int(rng.integers(0, 1 << 24))))
+                    msn=int(rng.integers(0, 1 << 24)),
+                    swap=int(rng.integers(0, 1 << 63)) * 2 + 1, comp=int(rng.integers(0, 1 << 63))))
     return wrs

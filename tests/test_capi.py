@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_errors():
     lib = E.load_library()
-    assert lib.ricrc_abi_version() == 2
+    assert lib.ricrc_abi_version() == 3
     assert lib.ricrc_strerror(0) == b"ok"
     assert lib.ricrc_strerror(-22) == b"invalid argument"
     assert lib.ricrc_strerror(-19) == b"no usable gfx950 device"
@@ -50,9 +50,9 @@ def test_product_package_never_imports_the_oracle():
         assert "icrc_oracle" not in text and "liboracle" not in text, f
 
 
-def test_header_is_plain_c_and_links(tmp_path):
-    """include/roce_icrc.h compiles as C99 and a C program links the library
-    and calls it (no GPU needed: planning, errors, ENODEV without a device)."""
+def build_abi_consumer(tmp_path):
+    """Compile tests/c/abi_consumer.c as C99 against include/roce_icrc.h and
+    link it to the library (also used by the GPU run in test_gpu_capi.py)."""
     import shutil
     import subprocess
     from pathlib import Path
@@ -66,11 +66,21 @@ def test_header_is_plain_c_and_links(tmp_path):
                     str(root / "tests" / "c" / "abi_consumer.c"), "-L", str(lib.parent),
                     "-l:" + lib.name, "-Wl,-rpath," + str(lib.parent), "-o", str(exe)],
                    check=True)
+    return exe
+
+
+def test_header_is_plain_c_and_links(tmp_path):
+    """include/roce_icrc.h compiles as C99 and a C program links the library
+    and calls it (no GPU here: planning, errors, ENODEV without a device; the
+    GPU run of the same program is tests/test_gpu_capi.py)."""
+    import subprocess
+    exe = build_abi_consumer(tmp_path)
     torch = pytest.importorskip("torch")
     if torch.cuda.is_available():
-        pytest.skip("the run leg is for GPU-less hosts (device 0 would be initialised)")
+        pytest.skip("GPU visible: the run leg is tests/test_gpu_capi.py")
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
-    assert out.startswith("abi 2 ok: 4 packets, slot 4352"), out
+    assert out.startswith("abi 3 ok: 4 packets, slot 4352"), out
+    assert "gpu leg skipped" in out
 
 
 def test_descriptor_arrays_must_match():

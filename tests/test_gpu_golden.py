@@ -88,8 +88,9 @@ def test_odd_length_datagram_does_not_shift_the_batch(engine):
     """A stray datagram whose length is not a multiple of 4 (truncated UDP
     packet) in the middle of a receive batch: it fails, and every valid frame
     after it still verifies and is delivered (frames are packed at dword-aligned
-    offsets); emit_batch with an odd-length frame in the batch still writes the
-    right ICRC into the frames after it."""
+    offsets).  On the emit side an odd-length frame is refused with ValueError
+    instead of getting the engine's ICRC 0 (the reference would CRC it; its
+    own emit paths always pad, src/roce_util.py:187-199)."""
     R.set_engine(engine)
     pkts = [R.l3_packet(R.BTH(opcode=0x01, psn=i, dqpn=0x30) / R.Raw(load=bytes([i]) * 64),
                         dst="10.0.0.2", sport=7, src="10.0.0.1") for i in range(8)]
@@ -104,8 +105,14 @@ def test_odd_length_datagram_does_not_shift_the_batch(engine):
     # emit side: a BTH/Raw build without padding gives an odd-length frame
     raw = R.IP(src="10.0.0.1", dst="10.0.0.2") / R.UDP(dport=4791, sport=7) / \
         R.BTH(opcode=0x04, psn=99, dqpn=0x30) / R.Raw(load=b"\x01\x02\x03")
-    mixed = R.emit_batch(pkts[:2] + [raw] + pkts[2:])
-    assert len(mixed[2]) % 4 == 3
+    with pytest.raises(ValueError, match="multiple of 4"):
+        R.emit_batch(pkts[:2] + [raw] + pkts[2:])
+    # padded as the reference's emit wrap pads it, the same packet goes through
+    padded = R.l3_packet(R.BTH(opcode=0x04, psn=99, dqpn=0x30) / R.Raw(load=b"\x01\x02\x03"),
+                         dst="10.0.0.2", sport=7, src="10.0.0.1")
+    mixed = R.emit_batch(pkts[:2] + [padded] + pkts[2:])
     assert mixed[:2] + mixed[3:] == frames
+    assert len(mixed[2]) % 4 == 0 and o.verify_frame(mixed[2])
+    assert mixed[2][-4:] == int(o.icrc_of_frame(mixed[2])).to_bytes(4, "little")
     for f in frames:
         assert o.verify_frame(f)

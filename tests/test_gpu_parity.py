@@ -410,6 +410,41 @@ def test_strided_tail_claims_concurrent_streams(engine):
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
 
 
+def test_claim_counters_never_shared_by_concurrent_launches(engine):
+    """One long strided launch on stream A while more than 64 short launches of
+    the SAME context go to three other streams (3 does not divide the 64 claim
+    slots): a launch must never find its tail-claim counters overwritten by a
+    launch in flight on another stream (which would leave its tail sets
+    unprocessed and their words stale).  Every output against the oracle."""
+    torch = pytest.importorskip("torch")
+    n_long = 1 << 20
+    buf, stride, flen = synth.uniform_frames(n_long, 4096, seed=77)
+    want_long, _ = oracle_batch(buf, stride=stride, length=flen, n=n_long)
+    d_long = torch.from_numpy(buf).cuda()
+    del buf
+    shorts = []
+    for i, n in enumerate([8 * 256 * 4 + 1, 8 * 256 * 4 + 77, 3 * 8 * 256 + 5]):
+        b, s_, f_ = synth.uniform_frames(n, 4096, seed=80 + i)
+        w, _ = oracle_batch(b, stride=s_, length=f_, n=n)
+        shorts.append((torch.from_numpy(b).cuda(), s_, f_, n, w))
+    out_long = torch.full((n_long,), -1, dtype=torch.int32, device="cuda")
+    outs = [torch.full((n,), -1, dtype=torch.int32, device="cuda") for *_, n, _ in shorts]
+    sa = torch.cuda.Stream()
+    ss = [torch.cuda.Stream() for _ in shorts]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        out_long.fill_(-1)
+        torch.cuda.synchronize()
+        engine.compute_strided_dev(d_long, stride, flen, n_long, out_long, stream=sa.cuda_stream)
+        for _ in range(30):  # 90 short launches behind the long one
+            for (d, s_, f_, n, _), out, st in zip(shorts, outs, ss):
+                engine.compute_strided_dev(d, s_, f_, n, out, stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out_long.cpu().numpy().view(np.uint32), want_long)
+        for (*_, w), out in zip(shorts, outs):
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), w)
+
+
 def test_multi_context_round_robin(engine):
     from roce_icrc import IcrcEngine, compute_batch_multi
     n = 3001

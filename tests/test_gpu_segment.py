@@ -108,7 +108,7 @@ def test_device_call_flags_bad_wrs(engine):
     npkts, slot = E.segment_plan(rec, pmtu)
     rec2 = np.concatenate([rec, to_records([wrs[0]])])
     rec2[2]["first_pkt"] = npkts
-    rec2[2]["op"] = 9
+    rec2[2]["op"] = E.SEG_NUM_OPS
     npkts += 1
     dev = torch.device("cuda", 0)
     d_mr = torch.from_numpy(mr).to(dev)
@@ -278,3 +278,100 @@ def test_mr_offsets_beyond_4_gib(engine):
         assert icrc[p] == O.icrc_of_frame(f), p
     del d_mr
     torch.cuda.empty_cache()
+
+
+def test_header_only_ops_match_packet_api(engine):
+    """Read request, CompareSwap / FetchAdd, ACK, RNR NAK, sequence and error
+    NAKs and the atomic acknowledge built by the kernel equal what the
+    packet-object mirror builds for the reference's own calls
+    (src/roce_sq.py:1421-1463, src/roce_rq.py:517-524, 767-853)."""
+    from roce_icrc import roce as R
+
+    va, rkey, swap, comp = 0x7F00AA5500001000, 0x1234ABCD, 0x0102030405060708, 0xFFEEDDCCBBAA9988
+    common = dict(mr_offset=0, dqpn=0x2A, src_ip=SRC_IP, dst_ip=DST_IP, sport=0x11)
+    wrs = [SO.SegWR(op=SO.READ_REQUEST, length=70000, psn=10, remote_va=va, rkey=rkey, **common),
+           SO.SegWR(op=SO.COMPARE_SWAP, length=0, psn=11, remote_va=va, rkey=rkey, swap=swap,
+                    comp=comp, **common),
+           SO.SegWR(op=SO.FETCH_ADD, length=0, psn=12, remote_va=va + 8, rkey=rkey, swap=0,
+                    comp=5, **common),
+           SO.SegWR(op=SO.ACK, length=0, psn=13, msn=3, **common),
+           SO.SegWR(op=SO.RNR_NAK, length=0, psn=14, msn=4, imm=9, **common),
+           SO.SegWR(op=SO.NAK, length=0, psn=15, msn=5, imm=0, **common),
+           SO.SegWR(op=SO.NAK, length=0, psn=16, msn=6, imm=2, **common),
+           SO.SegWR(op=SO.ATOMIC_ACK, length=0, psn=17, msn=7, swap=0xDEADBEEF00C0FFEE, **common)]
+    frames, lens, icrc, st = engine.segment(b"", to_records(wrs), 1024)
+    assert not st.any() and frames.shape[0] == len(wrs)
+
+    def wrap(p):
+        return R.l3_packet(p, dst="10.1.1.15", sport=0x11, src="10.1.1.48")
+    pkts = [
+        wrap(R.BTH(opcode=0x0C, psn=10, dqpn=0x2A, ackreq=True) / R.RETH(va=va, rkey=rkey,
+                                                                         dlen=70000)),
+        wrap(R.BTH(opcode=0x13, psn=11, dqpn=0x2A, ackreq=True)
+             / R.AtomicETH(va=va, rkey=rkey, comp=comp, swap=swap)),
+        wrap(R.BTH(opcode=0x14, psn=12, dqpn=0x2A, ackreq=True)
+             / R.AtomicETH(va=va + 8, rkey=rkey, comp=5, swap=0)),
+        wrap(R.BTH(opcode=0x11, psn=13, dqpn=0x2A) / R.AETH(code="ACK", value=31, msn=3)),
+        wrap(R.BTH(opcode=0x11, psn=14, dqpn=0x2A) / R.AETH(code="RNR", value=9, msn=4)),
+        wrap(R.BTH(opcode=0x11, psn=15, dqpn=0x2A) / R.AETH(code="NAK", value=0, msn=5)),
+        wrap(R.BTH(opcode=0x11, psn=16, dqpn=0x2A) / R.AETH(code="NAK", value=2, msn=6)),
+        wrap(R.BTH(opcode=0x12, psn=17, dqpn=0x2A) / R.AETH(code="ACK", value=31, msn=7)
+             / R.AtomicAckETH(orig=0xDEADBEEF00C0FFEE)),
+    ]
+    emitted = R.emit_batch(pkts)
+    want = SO.segment(b"", wrs, 1024)
+    for p, f in enumerate(emitted):
+        assert bytes(f) == want[p], p
+        assert frames[p, : lens[p]].tobytes() == bytes(f), p
+        assert icrc[p] == O.icrc_of_frame(f)
+
+
+@pytest.mark.parametrize("lanes", (0, 2, 16))
+def test_mixed_burst_is_one_launch_without_an_mr(engine, lanes):
+    """A responder-style burst -- read responses, ACKs, NAKs, atomic acks --
+    interleaved with requester packets in ONE ricrc_segment_dev call (one
+    segmentation launch); then a header-only burst with no MR at all (d_mr
+    NULL, mr_bytes 0).  Bit-exact against the oracle."""
+    import torch
+
+    pmtu = 256
+    rng = np.random.default_rng(21 + lanes)
+    mr = rng.integers(0, 256, 8 * pmtu + 3, dtype=np.uint8)
+    wrs = []
+    for i in range(300):
+        op = int(rng.integers(0, SO.ATOMIC_ACK + 1))
+        length = int(rng.integers(0, 3 * pmtu)) if op < SO.READ_REQUEST else int(rng.integers(0, 1 << 20))
+        off = int(rng.integers(0, mr.size - length + 1)) if op < SO.READ_REQUEST else 0
+        wrs.append(SO.SegWR(op=op, mr_offset=off, length=length, psn=int(rng.integers(0, 1 << 24)),
+                            dqpn=int(rng.integers(0, 1 << 24)), src_ip=SRC_IP, dst_ip=DST_IP,
+                            sport=int(rng.integers(0, 1 << 16)), flags=int(rng.integers(0, 4)),
+                            imm=int(rng.integers(0, 1 << 32)), remote_va=int(rng.integers(0, 1 << 63)),
+                            rkey=int(rng.integers(0, 1 << 32)), msn=int(rng.integers(0, 1 << 24)),
+                            swap=int(rng.integers(0, 1 << 63)), comp=int(rng.integers(0, 1 << 63))))
+    dev = torch.device("cuda", 0)
+    engine.set_lanes(lanes)
+    try:
+        for batch, use_mr in ((wrs, True), ([w for w in wrs if w.op in SO.HEADER_ONLY], False)):
+            rec = to_records(batch)
+            npkts, slot = E.segment_plan(rec, pmtu)
+            want = SO.segment(mr.tobytes(), batch, pmtu)
+            assert npkts == len(want)
+            d_mr = torch.from_numpy(mr).to(dev) if use_mr else None
+            d_wrs = torch.from_numpy(rec.view(np.uint8)).to(dev)
+            d_frames = torch.zeros(npkts * slot, dtype=torch.uint8, device=dev)
+            d_lens = torch.zeros(npkts, dtype=torch.int32, device=dev)
+            d_icrc = torch.zeros(npkts, dtype=torch.int32, device=dev)
+            d_st = torch.full((npkts,), 0xFF, dtype=torch.uint8, device=dev)
+            engine.segment_dev(d_mr, mr.size if use_mr else 0, d_wrs, len(batch), pmtu, npkts,
+                               d_frames, slot, d_lens, d_icrc, d_st)
+            torch.cuda.synchronize()
+            lens = d_lens.cpu().numpy().view(np.uint32)
+            icrc = d_icrc.cpu().numpy().view(np.uint32)
+            fr = d_frames.cpu().numpy().reshape(npkts, slot)
+            assert not d_st.cpu().numpy().any()
+            for p, f in enumerate(want):
+                assert lens[p] == len(f), p
+                assert fr[p, : len(f)].tobytes() == f, p
+                assert icrc[p] == O.icrc_of_frame(f), p
+    finally:
+        engine.set_lanes(0)

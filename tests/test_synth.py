@@ -31,6 +31,25 @@ def test_round_robin_shard_psns():
     assert sorted(seen) == list(range(world * 5))
 
 
+def test_cfg4_shards_are_the_one_global_stream():
+    """cfg4: ONE stream seeded 0x1C2C0004, packet i -> rank i mod N (SURVEY
+    8(d)); every rank's shard is exactly its rows of that stream."""
+    n_total, world = 37, 4
+    whole, stride, flen = synth.uniform_frames(n_total, 4096, seed=synth.SEED_CFG4)
+    rows = whole.reshape(n_total, flen)
+    got = {}
+    for rank in range(world):
+        buf, s, fl, idx = synth.shard_frames(n_total, rank, world, chunk=4)
+        assert s == fl == flen and list(idx) == list(range(rank, n_total, world))
+        sh = buf.reshape(-1, flen)
+        assert (sh == rows[idx]).all(), rank
+        for k, i in enumerate(idx):
+            got[int(i)] = R.IP(bytes(sh[k]))[R.BTH].psn
+    assert got == {i: i for i in range(n_total)}
+    one, _, _, idx = synth.shard_frames(n_total, 0, 1)
+    assert (one == whole).all() and idx.size == n_total
+
+
 def test_cfg3_mixed_mtu():
     n = 4000
     buf, offs, lens = synth.mixed_mtu_frames(n, seed=synth.SEED_CFG3)
