@@ -1123,8 +1123,17 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   auto fold4_masked = [&](int ihl, auto src) {
     return fold4([&](int k, int) { return fix_dword(src(k), k, ihl + 1, ihl + 3); });
   };
+  // Batches a wave loads are clamped to the workgroup's own staged range:
+  // the prefetch two rounds past its end re-reads the range's last batch
+  // (still in L2) instead of the next workgroup's first ones, which that
+  // workgroup reads again much later (an extra ~2.3 % of HBM reads at cfg5).
+  const uint32_t bs_end = min(b1, last);
   auto load = [&](uint32_t b, u32x4* Rg) {  // unconditional: clamped chunk index
+#ifdef RICRC_SMALL_OLD_CLAMP  // A/B switch: round-2 clamp (prefetch reaches the next range)
     const uint8_t* base = a.frames + (uint64_t)min(b, last - 1) * 64u * S;
+#else
+    const uint8_t* base = a.frames + (uint64_t)min(b, bs_end - 1u) * 64u * S;
+#endif
 #pragma unroll
     for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
   };
@@ -1178,10 +1187,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     __asm__ __volatile__("" ::: "memory");
   };
 
-  // staged batches [b0 + wave, min(b1, last)) step nw; each batch's
-  // loads are issued two batches ahead (buffers X, Y), right after the batch
-  // that used the buffer is staged (a third buffer measured no faster)
-  const uint32_t bs_end = min(b1, last);
+  // staged batches [b0 + wave, bs_end) step nw; each batch's loads are
+  // issued two batches ahead (buffers X, Y), right after the batch that used
+  // the buffer is staged (a third buffer measured no faster)
   if (kRing && rounds_cap > 0 && b0 < bs_end) {  // (uniform)
     // rounds: round r is batch b0 + r nw + wave of every wave (waves past
     // bs_end recompute a clamped batch and emit nothing); every rounds_cap
