@@ -93,9 +93,19 @@ void* ricrc_ctx_stream(ricrc_ctx* ctx);
 
 /* ---- host buffers, synchronous (H2D + kernel + D2H) --------------------- */
 /* The per-packet drop-in for BTH.compute_icrc (src/roce.py:192): one wire
- * frame in, its ICRC out (runs on the GPU through the context's scratch). */
+ * frame in, its ICRC out.  By default it goes through the context's
+ * per-packet service: one resident GPU wave polling a request slot in pinned
+ * host memory, which reads the frame over PCIe and answers in host memory --
+ * no kernel launch, copy or stream synchronisation per call.  The wave is
+ * launched by the first call and leaves after `idle_us` without a call, when
+ * the context launches batch work (it holds one CU's LDS while it runs), or
+ * when the context is destroyed.  Frames over 64 KiB, or a context whose
+ * service is off, take one staged kernel launch per call instead. */
 int ricrc_compute_one(ricrc_ctx* ctx, const uint8_t* frame, size_t len, uint32_t* icrc_out,
                       uint8_t* status_out /* nullable */);
+/* Idle timeout of the per-packet service in microseconds (default 1000);
+ * 0 turns the service off (ricrc_compute_one then launches a kernel per call). */
+int ricrc_ctx_set_service(ricrc_ctx* ctx, uint32_t idle_us);
 
 /* Ragged batch: frame i is frames[offsets[i] .. offsets[i] + lens[i]).
  * `frames_bytes` is the size of the `frames` buffer (bounds for the copy). */

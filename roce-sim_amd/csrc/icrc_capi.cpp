@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -54,6 +56,14 @@ struct ricrc_ctx {
   // its device twin, so a call is one H2D copy, one kernel, one D2H copy
   uint8_t* h_stage = nullptr;
   uint8_t* d_stage = nullptr;
+  // per-packet service (ricrc_compute_one): request slot in pinned
+  // fine-grained host memory, the stream its resident wave runs on
+  ricrc::ServiceRing* svc = nullptr;
+  hipStream_t svc_stream = nullptr;
+  bool svc_launched = false;
+  uint32_t svc_seq = 0;
+  uint32_t svc_idle_us = 1000;  // 0 = service off (staged launch per call)
+  std::chrono::steady_clock::time_point svc_last{};  // last call (the wave's idle clock)
 };
 
 namespace {
@@ -182,9 +192,17 @@ unsigned long long* claim_region(ricrc_ctx* c, hipStream_t s, uint32_t* epoch) {
   return c->d_claims + r * (size_t)ricrc::kClaimSlots * ricrc::kMaxClaimBlocks;
 }
 
+// The per-packet service's wave holds one CU's LDS while it runs: a context
+// about to launch batch work asks it to leave first (it does within a few
+// microseconds; the next ricrc_compute_one relaunches it).
+void service_pause(ricrc_ctx* c) {
+  if (c->svc_launched) __atomic_store_n(&c->svc->stop, 1u, __ATOMIC_RELEASE);
+}
+
 int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint32_t* lens,
            uint64_t stride, uint32_t len, uint32_t n, uint32_t* icrc, uint8_t* status, uint8_t* ok,
            bool ragged, bool verify, int log2g, hipStream_t s) {
+  service_pause(c);
   ricrc::IcrcArgs a{};
   a.frames = frames;
   a.offsets = offs;
@@ -357,8 +375,129 @@ int seg_launch(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes, const ricrc
   a.icrc_out = d_icrc;
   a.status_out = d_status;
   a.tables = c->d_tables;
+  service_pause(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(ricrc::launch_segment(a, seg_log2g(c, pmtu), c->num_cus, s));
+  return RICRC_OK;
+}
+
+// ---- per-packet service (see icrc_service_kernel) --------------------------
+
+// Every context whose service may be running, so that process exit stops
+// them before the HIP runtime tears down (a resident wave must not outlive
+// the host memory it polls).
+std::mutex g_svc_mu;
+std::vector<ricrc_ctx*> g_svc_ctxs;
+bool g_svc_atexit = false;
+
+void service_stop_wait(ricrc_ctx* c) {
+  if (!c->svc_launched) return;
+  __atomic_store_n(&c->svc->stop, 1u, __ATOMIC_RELEASE);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->svc_stream);
+  c->svc_launched = false;
+}
+
+void service_atexit() {
+  std::lock_guard<std::mutex> lk(g_svc_mu);
+  for (ricrc_ctx* c : g_svc_ctxs) service_stop_wait(c);
+  g_svc_ctxs.clear();
+}
+
+int service_init(ricrc_ctx* c) {
+  if (c->svc) return RICRC_OK;
+  void* h = nullptr;
+  HIP_TRY(hipHostMalloc(&h, ricrc::kSvcBytes, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(h, 0, sizeof(ricrc::ServiceRing));
+  hipError_t e = hipStreamCreateWithFlags(&c->svc_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return hip_fail(e);
+  }
+  c->svc = (ricrc::ServiceRing*)h;
+  std::lock_guard<std::mutex> lk(g_svc_mu);
+  g_svc_ctxs.push_back(c);
+  if (!g_svc_atexit) {
+    std::atexit(service_atexit);
+    g_svc_atexit = true;
+  }
+  return RICRC_OK;
+}
+
+void service_forget(ricrc_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_svc_mu);
+  for (size_t i = 0; i < g_svc_ctxs.size(); ++i)
+    if (g_svc_ctxs[i] == c) {
+      g_svc_ctxs.erase(g_svc_ctxs.begin() + (long)i);
+      break;
+    }
+}
+
+// (Re)launch the wave if it is not running: it left after a stop request or
+// its idle timeout, or never ran.
+int service_ensure(ricrc_ctx* c) {
+  const auto now = std::chrono::steady_clock::now();
+  if (c->svc_launched && __atomic_load_n(&c->svc->stop, __ATOMIC_ACQUIRE) == 0u) {
+    // called again well within the idle timeout: the wave is still there
+    // (no runtime query on the fast path); later, ask the stream
+    if (now - c->svc_last < std::chrono::microseconds(c->svc_idle_us / 2) ||
+        hipStreamQuery(c->svc_stream) == hipErrorNotReady) {
+      c->svc_last = now;
+      return RICRC_OK;
+    }
+  }
+  c->svc_last = now;
+  HIP_TRY(hipStreamSynchronize(c->svc_stream));  // a leaving wave has left
+  ricrc::ServiceRing* r = c->svc;
+  __atomic_store_n(&r->stop, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&r->exited, 0u, __ATOMIC_RELAXED);
+  ricrc::ServiceArgs a{};
+  a.ring = r;  // (unified addressing: the mapped host pointer is the device pointer)
+  a.tables = c->d_tables;
+  a.served = __atomic_load_n(&r->req_seq, __ATOMIC_ACQUIRE);
+  a.idle_ticks = (uint64_t)c->svc_idle_us * 100u;  // 100 MHz real-time counter
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  HIP_TRY(ricrc::launch_service(a, c->svc_stream));
+  c->svc_launched = true;
+  return RICRC_OK;
+}
+
+// One frame through the resident wave.  Returns RICRC_EIO (with the service
+// stopped) if no answer came within a second -- the caller then takes the
+// launch path.
+int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icrc_out,
+                 uint8_t* status_out) {
+  int rc = service_init(c);
+  if (rc) return rc;
+  rc = service_ensure(c);
+  if (rc) return rc;
+  ricrc::ServiceRing* r = c->svc;
+  std::memcpy((uint8_t*)r + ricrc::kSvcFrame, frame, len);
+  r->len = len;
+  const uint32_t seq = ++c->svc_seq == 0 ? ++c->svc_seq : c->svc_seq;  // (0 = nothing yet)
+  __atomic_store_n(&r->req_seq, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(&r->resp_seq, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spin & 255u) == 0) {
+      // the wave may have left (idle timeout) just before the request was
+      // published: once its stream is idle and the answer is still missing,
+      // launch it again (it serves the pending request first)
+      if (hipStreamQuery(c->svc_stream) == hipSuccess &&
+          __atomic_load_n(&r->resp_seq, __ATOMIC_ACQUIRE) != seq) {
+        c->svc_launched = false;
+        rc = service_ensure(c);
+        if (rc) return rc;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+        service_stop_wait(c);
+        return RICRC_EIO;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  *icrc_out = r->icrc;
+  if (status_out) *status_out = (uint8_t)r->status;
   return RICRC_OK;
 }
 
@@ -423,6 +562,10 @@ int ricrc_ctx_create(int device, ricrc_ctx** out) {
 
 void ricrc_ctx_destroy(ricrc_ctx* c) {
   if (!c) return;
+  if (c->svc) {
+    service_forget(c);
+    service_stop_wait(c);
+  }
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   (void)hipFree(c->d_tables);
@@ -437,6 +580,8 @@ void ricrc_ctx_destroy(ricrc_ctx* c) {
   (void)hipFree(c->d_wrs);
   (void)hipFree(c->d_stage);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->svc) (void)hipHostFree(c->svc);
+  if (c->svc_stream) (void)hipStreamDestroy(c->svc_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -455,9 +600,22 @@ int ricrc_lanes_for_len(ricrc_ctx* c, uint32_t len) {
   return 1 << pick_log2g(c, len);
 }
 
+int ricrc_ctx_set_service(ricrc_ctx* c, uint32_t idle_us) {
+  if (!c || idle_us > 10000000u) return RICRC_EINVAL;
+  if (idle_us == 0 && c->svc) service_stop_wait(c);
+  c->svc_idle_us = idle_us;
+  if (c->svc_launched) service_pause(c);  // the next call relaunches with the new timeout
+  return RICRC_OK;
+}
+
 int ricrc_compute_one(ricrc_ctx* c, const uint8_t* frame, size_t len, uint32_t* icrc_out,
                       uint8_t* status_out) {
   if (!c || !frame || !icrc_out || len > 0xFFFFFFFFull) return RICRC_EINVAL;
+  if (c->svc_idle_us && len <= ricrc::kSvcMaxFrame) {
+    HIP_TRY(hipSetDevice(c->device));
+    const int rc = service_call(c, frame, (uint32_t)len, icrc_out, status_out);
+    if (rc != RICRC_EIO) return rc;  // (no answer within 1 s: the launch path below)
+  }
   const uint64_t off = 0;
   const uint32_t l = (uint32_t)len;
   return host_ragged(c, frame, len, &off, &l, 1, icrc_out, status_out, nullptr, false);
@@ -612,6 +770,7 @@ int ricrc_stream_read_dev(ricrc_ctx* c, const uint8_t* d_buf, uint64_t bytes, ui
                           void* stream) {
   if (!c || !d_buf || !d_sink || (bytes & 15)) return RICRC_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
+  service_pause(c);
   HIP_TRY(ricrc::launch_stream_read(d_buf, bytes, d_sink, c->num_cus, pick_stream(c, stream)));
   return RICRC_OK;
 }
@@ -704,6 +863,7 @@ int ricrc_inject_faults_dev(ricrc_ctx* c, uint8_t* d_frames, const uint64_t* d_o
   a.kinds = kinds;
   a.fault_out = d_fault_out;
   HIP_TRY(hipSetDevice(c->device));
+  service_pause(c);
   HIP_TRY(ricrc::launch_faults(a, c->num_cus, pick_stream(c, stream)));
   return RICRC_OK;
 }
@@ -712,6 +872,7 @@ int ricrc_stream_copy_dev(ricrc_ctx* c, const uint8_t* d_src, uint8_t* d_dst, ui
                           void* stream) {
   if (!c || !d_src || !d_dst || (bytes & 15)) return RICRC_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
+  service_pause(c);
   HIP_TRY(ricrc::launch_stream_copy(d_src, d_dst, bytes, c->num_cus, pick_stream(c, stream)));
   return RICRC_OK;
 }

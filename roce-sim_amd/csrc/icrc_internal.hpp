@@ -92,6 +92,35 @@ hipError_t launch_stream_copy(const uint8_t* src, uint8_t* dst, uint64_t bytes, 
 
 namespace ricrc {
 
+// Per-packet service (icrc_kernels.hip, icrc_service_kernel): the request /
+// response slot in pinned fine-grained host memory.  Host-written words and
+// GPU-written words sit on separate 128-byte lines; the frame at kSvcFrame.
+struct ServiceRing {
+  uint32_t req_seq;  // host: published (release) after len and the frame
+  uint32_t len;      // host: frame bytes incl. the ICRC slot
+  uint32_t stop;     // host: 1 = leave now
+  uint32_t pad0[29];
+  uint32_t resp_seq;  // GPU: = req_seq once icrc / status hold its result
+  uint32_t icrc;
+  uint32_t status;
+  uint32_t exited;  // GPU: 1 when the wave has left its loop
+  uint32_t pad1[28];
+};
+constexpr uint32_t kSvcFrame = 1024;  // frame offset in the slot (aligned grid: 1 KiB at G = 64)
+constexpr uint32_t kSvcMaxFrame = 65536;
+constexpr size_t kSvcBytes = kSvcFrame + kSvcMaxFrame;
+static_assert(sizeof(ServiceRing) == 256, "two 128-byte lines");
+
+struct ServiceArgs {
+  ServiceRing* ring;  // device view of the host slot
+  const uint32_t* tables;
+  uint32_t served;      // last request sequence number already answered
+  uint64_t idle_ticks;  // 100 MHz ticks without a request before the wave leaves
+};
+
+// Enqueues the service kernel (one workgroup) on `stream`.
+hipError_t launch_service(const ServiceArgs& a, hipStream_t stream);
+
 struct FaultArgs {
   uint8_t* frames;
   const uint64_t* offsets;

@@ -1285,6 +1285,73 @@ __global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4
   if (x == 0x9E3779B9u) sink[0] = x;  // keeps the loads live; practically never stores
 }
 
+// ---------------------------------------------------------------------------
+// Per-packet service: the low-latency form of ricrc_compute_one (the
+// drop-in for BTH.compute_icrc, src/roce.py:192-223, one frame per call).
+//
+// A launched kernel costs more than the CRC of one frame (launch, copies and
+// a stream synchronisation put a plain call at ~25 us, where zlib.crc32 needs
+// ~4 us for 4 KiB).  Here ONE wave stays resident and polls a request slot in
+// pinned fine-grained host memory (ServiceRing, icrc_internal.hpp): the host
+// copies the frame into the slot and publishes a sequence number; the wave
+// sees it, reads the frame straight from host memory over PCIe (64 lanes,
+// one 16-byte load each per KiB, all in flight at once), folds it with the
+// batch kernels' 64-lane group code (Mul(8192) tables in LDS, butterfly
+// combine) and writes the ICRC, the status and the sequence number back into
+// host memory, where the caller spins on it.
+//
+// Polling uses relaxed system-scope loads (no cache maintenance per poll);
+// one acquire fence per request makes the frame bytes the host wrote before
+// publishing visible, one release fence publishes the result before the
+// sequence number.  The wave leaves when the host raises `stop` (context
+// destroyed, or about to launch batch work, which needs this CU's LDS) or
+// after `idle_ticks` of the 100 MHz real-time counter without a request:
+// every path through the loop reaches one of the two, so the grid always
+// drains; the host relaunches it on the next call.
+constexpr int kSvcThreads = 256;  // all stage the tables; wave 0 then serves
+__global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArgs s) {
+  constexpr int LOG2G = 6;
+  constexpr int DPI = 4 << LOG2G;
+  const int tid = threadIdx.x;
+  stage_tables<LOG2G, kSvcThreads, MainKeys>(s.tables, tid);
+  __syncthreads();
+  if (tid >= 64) return;
+  const int lane = tid;
+  const MainKeys kk = MainKeys::make(lane);
+  ServiceRing* r = s.ring;
+  const uint8_t* frame = (const uint8_t*)r + kSvcFrame;
+  IcrcArgs a{};
+  a.frames = frame;
+  a.n = 1;
+  a.icrc_out = &r->icrc;
+  a.status_out = (uint8_t*)&r->status;  // (the low byte of the word, little-endian)
+  uint32_t served = s.served;
+  uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(&r->req_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (seq != served) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before seq
+      const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)__hip_atomic_load(&r->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      const Pkt p = describe<DPI>(frame, 0, true, 0, L <= kSvcMaxFrame ? L : 0u);
+      Batch<kUnroll> b = issue_packet<LOG2G, false>(p, lane);
+      finish_packet<LOG2G, false>(a, p, b, lane, 0, kk);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // icrc / status before the sequence number
+      if (lane == 0) __hip_atomic_store(&r->resp_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      served = seq;
+      t_last = __builtin_amdgcn_s_memrealtime();
+      continue;
+    }
+    if (__hip_atomic_load(&r->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+    if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane == 0) __hip_atomic_store(&r->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+constexpr size_t kSvcLds = kFixLut<6, MainKeys> + 256u;  // tables + combine sets + fix-up LUT
+
 typedef void (*kernel_fn)(IcrcArgs);
 
 template <int LOG2G>
@@ -1361,7 +1428,15 @@ hipError_t prepare_kernels() {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
         if (e != hipSuccess) return e;
       }
+  hipError_t e = hipFuncSetAttribute((const void*)icrc_service_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSvcLds);
+  if (e != hipSuccess) return e;
   return prepare_segment_kernels();
+}
+
+hipError_t launch_service(const ServiceArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(icrc_service_kernel, dim3(1), dim3(kSvcThreads), kSvcLds, stream, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,

@@ -6,6 +6,9 @@ Submodules:
   roce    -- the reference's packet-object API (BTH, AETH, ... , IP, UDP)
              with ICRC compute/verify routed through the engine
   synth   -- synthetic frame batches for the BASELINE.json configurations
+  recv    -- the receive loop: datagram sources (raw socket, pcap, memory)
+             batched through the GPU ICRC verify, dispatch like recv_pkts
+  hooks   -- reference-shaped SEND/RESP hooks for ICRC fault injection
 """
 
 from .engine import (  # noqa: F401

@@ -79,6 +79,7 @@ _SIGNATURES = {
     "ricrc_ctx_destroy": (None, [_vp]),
     "ricrc_ctx_set_lanes_per_packet": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ricrc_ctx_stream": (_vp, [_vp]),
+    "ricrc_ctx_set_service": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "ricrc_compute_one": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, _vp]),
     "ricrc_compute_batch": (
         ctypes.c_int,
@@ -244,6 +245,8 @@ class IcrcEngine:
             raise IcrcUnavailable(f"ricrc_ctx_create({device}) -> {rc} ({self._msg(rc)})")
         self.ctx = ctx
         self.device = device
+        self._one, self._one_st = ctypes.c_uint32(0), ctypes.c_uint8(0)  # compute_one outputs
+        self._one_ref, self._one_st_ref = ctypes.byref(self._one), ctypes.byref(self._one_st)
         if lanes:
             self.set_lanes(lanes)
 
@@ -276,6 +279,11 @@ class IcrcEngine:
         self._check("ricrc_ctx_set_lanes_per_packet",
                     self.lib.ricrc_ctx_set_lanes_per_packet(self.ctx, lanes))
 
+    def set_service(self, idle_us: int) -> None:
+        """Idle timeout of the per-packet service behind compute_one (0 = off:
+        one kernel launch per call)."""
+        self._check("ricrc_ctx_set_service", self.lib.ricrc_ctx_set_service(self.ctx, idle_us))
+
     def lanes_for_len(self, length: int) -> int:
         return self.lib.ricrc_lanes_for_len(self.ctx, length)
 
@@ -285,13 +293,18 @@ class IcrcEngine:
 
     # -- host buffers (synchronous) ----------------------------------------
     def compute_one(self, frame) -> tuple[int, int]:
-        """Drop-in for BTH.compute_icrc (src/roce.py:192): wire frame -> (icrc, status)."""
-        f = _u8(frame)
-        out = np.zeros(1, np.uint32)
-        st = np.zeros(1, np.uint8)
-        self._check("ricrc_compute_one",
-                    self.lib.ricrc_compute_one(self.ctx, _ptr(f), f.size, _ptr(out), _ptr(st)))
-        return int(out[0]), int(st[0])
+        """Drop-in for BTH.compute_icrc (src/roce.py:192): wire frame -> (icrc, status).
+        One ctypes call (bytes pass without a copy; the outputs are reused
+        ctypes scalars), served by the context's per-packet GPU service."""
+        if isinstance(frame, bytes):
+            ptr, n = frame, len(frame)
+        else:
+            f = _u8(frame)
+            ptr, n = _ptr(f), f.size
+        rc = self.lib.ricrc_compute_one(self.ctx, ptr, n, self._one_ref, self._one_st_ref)
+        if rc != RICRC_OK:
+            self._check("ricrc_compute_one", rc)
+        return self._one.value, self._one_st.value
 
     def compute_batch(self, frames, offsets, lens):
         f = _u8(frames)

@@ -1,0 +1,298 @@
+"""Receive loop: datagram sources feeding the GPU ICRC verify in batches.
+
+Reference receive loops (read as text; datenlord/roce-sim):
+  ``RoCEv2.recv_pkts``   src/roce_v2.py:327-372
+  ``RXLogic.recv_pkts``  src/roce_rq.py:877-931
+Both call ``recvfrom(UDP_BUF_SIZE)`` on a SOCK_DGRAM socket bound to UDP 4791
+(src/roce_v2.py:269-271, 348; src/roce_rq.py:899), dissect ``BTH(roce_bytes)``
+and hand each packet to ``QP.recv_pkt`` (src/roce_v2.py:181-231), skipping
+packets for other QPs when ``qpn`` is given.  Two limits follow from that
+socket: the IPv4 header the ICRC covers is never
+seen, so nothing is verified, and ``UDP_BUF_SIZE = 1024`` (src/roce_enum.py:6)
+truncates every larger datagram.
+
+Here the loop reads whole IPv4 datagrams (no size cap) from a source,
+verifies a whole batch of them with ONE GPU call (``verify_frames``: the
+``ricrc_verify_batch`` kernel), drops the frames whose ICRC does not match --
+what Linux rxe, the reference's CI peer, does -- and dispatches the rest
+exactly as the reference loop does, one layer below ``recv_pkt`` /
+``verify_pkt_head`` (src/roce_v2.py:171-192).
+
+Sources:
+  ``RawSocketSource``  AF_INET/SOCK_RAW/IPPROTO_UDP socket: every UDP datagram
+                       to this host with its IPv4 header; non-RoCE ports are
+                       skipped.  Needs CAP_NET_RAW (as scapy's ``send()`` of
+                       the reference's emit path does).
+  ``PcapSource``       a capture file (LINKTYPE_RAW / IPV4 / ETHERNET).
+  ``ListSource``       datagrams already in memory.
+``RawIpSink`` is the emit side (IP_HDRINCL raw socket, the L3 ``send()`` of
+src/roce_sq.py:1197 and src/roce_rq.py:731) for frames built by ``emit_batch``
+or the GPU segmentation.
+"""
+from __future__ import annotations
+
+import errno
+import logging
+import socket
+import struct
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Iterable, Optional
+
+from .roce import BTH, ROCE_PORT, verify_frames
+
+MAX_DATAGRAM = 65535  # an IPv4 datagram, no 1024-byte cap (src/roce_enum.py:6)
+
+
+def roce_udp_dport(dgram: bytes) -> Optional[int]:
+    """UDP destination port of an IPv4/UDP datagram, or None."""
+    if len(dgram) < 20 or dgram[0] >> 4 != 4 or dgram[9] != 17:
+        return None
+    ihl = 4 * (dgram[0] & 0xF)
+    if len(dgram) < ihl + 8:
+        return None
+    return struct.unpack_from("!H", dgram, ihl + 2)[0]
+
+
+class ListSource:
+    """Datagrams already in memory, handed out in order."""
+
+    def __init__(self, datagrams: Iterable[bytes]):
+        self._q = list(datagrams)
+        self._i = 0
+
+    def recv_batch(self, max_n: int, timeout: Optional[float]) -> list[bytes]:
+        if self._i >= len(self._q):
+            raise socket.timeout("no more datagrams")
+        out = self._q[self._i:self._i + max_n]
+        self._i += len(out)
+        return out
+
+    def close(self):
+        pass
+
+
+class RawSocketSource:
+    """Whole IPv4 datagrams of every UDP packet this host receives; the loop
+    keeps those to ``port``.  The first datagram of a batch is waited for
+    (``timeout`` like the reference's ``settimeout``), the rest of the batch
+    is whatever has already arrived (non-blocking drain)."""
+
+    def __init__(self, port: int = ROCE_PORT, bind_addr: str = "0.0.0.0"):
+        self.port = port
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_RAW, socket.IPPROTO_UDP)
+        self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 64 << 20)
+        if bind_addr != "0.0.0.0":
+            self.sock.bind((bind_addr, 0))
+        self._buf = bytearray(MAX_DATAGRAM)
+
+    def _recv(self, flags: int) -> Optional[bytes]:
+        n = self.sock.recv_into(self._buf, MAX_DATAGRAM, flags)
+        d = bytes(self._buf[:n])
+        return d if roce_udp_dport(d) == self.port else None
+
+    def recv_batch(self, max_n: int, timeout: Optional[float]) -> list[bytes]:
+        out: list[bytes] = []
+        deadline = None if timeout is None else time.monotonic() + timeout
+        while not out:  # the first RoCE datagram, within the timeout
+            left = None if deadline is None else deadline - time.monotonic()
+            if left is not None and left <= 0:
+                raise socket.timeout("timed out")
+            self.sock.settimeout(left)
+            d = self._recv(0)
+            if d is not None:
+                out.append(d)
+        self.sock.settimeout(0.0)  # then whatever is queued already
+        while len(out) < max_n:
+            try:
+                d = self._recv(0)
+            except (BlockingIOError, InterruptedError, socket.timeout):
+                break
+            except OSError as e:
+                if e.errno in (errno.EAGAIN, errno.EWOULDBLOCK):
+                    break
+                raise
+            if d is not None:
+                out.append(d)
+        return out
+
+    def close(self):
+        self.sock.close()
+
+
+class RawIpSink:
+    """Sends complete IPv4 frames as built (IP_HDRINCL): the L3 ``send()`` the
+    reference calls at src/roce_sq.py:1197 and src/roce_rq.py:731, for frames
+    whose ICRC the GPU computed (``emit_batch``, ``ricrc_segment``)."""
+
+    def __init__(self):
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_RAW, socket.IPPROTO_RAW)
+        self.sock.setsockopt(socket.IPPROTO_IP, socket.IP_HDRINCL, 1)
+        self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 64 << 20)
+
+    def send(self, frames: Iterable[bytes]) -> int:
+        n = 0
+        for f in frames:
+            dst = socket.inet_ntoa(f[16:20])
+            self.sock.sendto(f, (dst, 0))
+            n += 1
+        return n
+
+    def close(self):
+        self.sock.close()
+
+
+# pcap: the classic libpcap file format (24-byte
+# global header, 16-byte record headers), microsecond or nanosecond magic
+_PCAP_MAGIC = {0xA1B2C3D4: ("<", 1e-6), 0xD4C3B2A1: (">", 1e-6),
+               0xA1B23C4D: ("<", 1e-9), 0x4D3CB2A1: (">", 1e-9)}
+LINKTYPE_ETHERNET, LINKTYPE_RAW, LINKTYPE_IPV4 = 1, 101, 228
+
+
+def write_pcap(path, datagrams: Iterable[bytes], linktype: int = LINKTYPE_RAW) -> int:
+    """Write IPv4 datagrams as a capture file (LINKTYPE_RAW)."""
+    n = 0
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, MAX_DATAGRAM + 14, linktype))
+        for d in datagrams:
+            if linktype == LINKTYPE_ETHERNET:
+                d = b"\x02\0\0\0\0\x02" + b"\x02\0\0\0\0\x01" + b"\x08\x00" + d
+            f.write(struct.pack("<IIII", n, 0, len(d), len(d)) + d)
+            n += 1
+    return n
+
+
+class PcapSource:
+    """IPv4 datagrams from a capture file (raw-IP or Ethernet link type)."""
+
+    def __init__(self, path):
+        self._f = open(path, "rb")
+        hdr = self._f.read(24)
+        if len(hdr) < 24:
+            raise ValueError(f"{path}: not a pcap file")
+        magic = struct.unpack("<I", hdr[:4])[0]
+        if magic not in _PCAP_MAGIC:
+            raise ValueError(f"{path}: bad pcap magic {magic:#x}")
+        self._e = _PCAP_MAGIC[magic][0]
+        self.linktype = struct.unpack(self._e + "I", hdr[20:24])[0] & 0xFFFF
+        if self.linktype not in (LINKTYPE_ETHERNET, LINKTYPE_RAW, LINKTYPE_IPV4):
+            raise ValueError(f"{path}: link type {self.linktype} not supported")
+
+    def _next(self) -> Optional[bytes]:
+        while True:
+            rh = self._f.read(16)
+            if len(rh) < 16:
+                return None
+            _, _, incl, _ = struct.unpack(self._e + "IIII", rh)
+            d = self._f.read(incl)
+            if self.linktype == LINKTYPE_ETHERNET:
+                if len(d) < 14 or d[12:14] != b"\x08\x00":
+                    continue  # not IPv4
+                d = d[14:]
+            return d
+
+    def recv_batch(self, max_n: int, timeout: Optional[float]) -> list[bytes]:
+        out = []
+        while len(out) < max_n:
+            d = self._next()
+            if d is None:
+                break
+            out.append(d)
+        if not out:
+            raise socket.timeout("end of capture")
+        return out
+
+    def close(self):
+        self._f.close()
+
+
+@dataclass
+class RecvStats:
+    datagrams: int = 0      # datagrams taken from the source
+    not_roce: int = 0       # not IPv4/UDP to the RoCE port
+    icrc_dropped: int = 0   # ICRC mismatch (dropped, as rxe does)
+    other_qp: int = 0       # skipped: dqpn != qpn (src/roce_v2.py:359-364)
+    delivered: int = 0      # handed to the dispatch
+    gpu_calls: int = 0      # verify launches (one per batch)
+    dropped_frames: list = field(default_factory=list)  # the datagrams dropped for their ICRC
+
+
+class RecvLoop:
+    """Batches datagrams from ``source`` through the GPU ICRC verify and
+    dispatches the packets that pass, like the reference's ``recv_pkts``.
+
+    ``dispatch(bth) -> opcode`` receives each delivered packet as the ``BTH``
+    object the reference dissects (src/roce_v2.py:350, src/roce_rq.py:901) --
+    e.g. ``lambda p: qp_dict[p.dqpn].recv_pkt(p, retry_handler)``.
+    ``verify(frames) -> ok flags`` defaults to the GPU (``verify_frames``)."""
+
+    def __init__(self, source, dispatch: Optional[Callable[[BTH], object]] = None,
+                 batch: int = 1024, timeout: Optional[float] = 1.0,
+                 verify: Optional[Callable[[list], Iterable[bool]]] = None,
+                 keep_dropped: bool = False):
+        self.source = source
+        self.dispatch = dispatch
+        self.batch = batch
+        self.timeout = timeout
+        self.verify = verify or verify_frames
+        self.keep_dropped = keep_dropped
+        self.stats = RecvStats()
+        self._pending: list[BTH] = []  # verified packets not yet handed out
+
+    def _fill(self) -> None:
+        # up to `batch` datagrams per verify launch (the ones a source already
+        # holds; a raw socket waits only for the first)
+        dg = self.source.recv_batch(self.batch, self.timeout)
+        self.stats.datagrams += len(dg)
+        roce = [d for d in dg if roce_udp_dport(d) == ROCE_PORT]
+        self.stats.not_roce += len(dg) - len(roce)
+        if not roce:
+            return
+        ok = self.verify(roce)
+        self.stats.gpu_calls += 1
+        for d, good in zip(roce, ok):
+            if not good:
+                self.stats.icrc_dropped += 1
+                if self.keep_dropped:
+                    self.stats.dropped_frames.append(d)
+                logging.info("dropped a RoCE datagram of %d bytes: ICRC mismatch", len(d))
+                continue
+            ihl = 4 * (d[0] & 0xF)
+            self._pending.append(BTH(d[ihl + 8:]))
+
+    def recv_pkts(self, npkt: int, qpn: Optional[int] = None,
+                  check_pkt: Optional[Callable[[BTH], bool]] = None):
+        """src/roce_v2.py:327-372 / src/roce_rq.py:877-931: receive ``npkt``
+        packets (skipping other QPs when ``qpn`` is set), return their opcodes
+        (the dispatch's return values when a dispatch is set).  ``npkt == 0``
+        expects the timeout and returns [].  A source running dry raises
+        ``socket.timeout`` as ``recvfrom`` does."""
+        if npkt == 0:
+            try:
+                self._fill()
+            except socket.timeout:
+                return []
+            raise AssertionError("BUG: just wait for timeout and it should not receive any packet")
+        out = []
+        while len(out) < npkt:
+            if not self._pending:
+                self._fill()
+                continue
+            pkt = self._pending.pop(0)
+            if qpn is not None and pkt.dqpn != qpn:
+                self.stats.other_qp += 1
+                logging.warning("expected qpn: %s, received pkt's qpn: %s", qpn, pkt.dqpn)
+                continue
+            if check_pkt is not None:
+                check_pkt(pkt)
+            self.stats.delivered += 1
+            out.append(self.dispatch(pkt) if self.dispatch else pkt.opcode)
+        return out
+
+    def packets(self, npkt: int, qpn: Optional[int] = None) -> list[BTH]:
+        """The next ``npkt`` verified packets themselves (no dispatch)."""
+        saved, self.dispatch = self.dispatch, (lambda p: p)
+        try:
+            return self.recv_pkts(npkt, qpn=qpn)
+        finally:
+            self.dispatch = saved

@@ -33,12 +33,32 @@ def main():
     ap.add_argument("--reps", type=int, default=300)
     a = ap.parse_args()
     eng = IcrcEngine(0)
-    for pay in (64, 1024, 4096):
-        buf, stride, flen = synth.uniform_frames(1, pay)
-        frame = bytes(buf[:flen])
-        med, p99 = med_us(lambda: eng.compute_one(frame), a.reps)
-        print(json.dumps({"call": "compute_one", "frame_bytes": flen, "median_us": round(med, 2),
-                          "p99_us": round(p99, 2)}), flush=True)
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import icrc_oracle as orc  # checker only: every timed answer is compared
+    for service in (1000, 0):  # the resident per-packet service, then one launch per call
+        eng.set_service(service)
+        for pay in (0, 64, 1024, 4096):
+            buf, stride, flen = synth.uniform_frames(1, pay)
+            frame = bytes(buf[:flen])
+            want = orc.icrc_of_frame(frame)
+            got = []
+            med, p99 = med_us(lambda: got.append(eng.compute_one(frame)[0]), a.reps)
+            assert set(got) == {want}, (hex(want), {hex(x) for x in got})
+            # the reference's own arithmetic on this host, per frame (zlib.crc32
+            # of the masked pseudo packet, src/roce.py:218), for scale
+            zmed, _ = med_us(lambda: orc.icrc_of_frame(frame), a.reps)
+            print(json.dumps({"call": "compute_one", "service_idle_us": service,
+                              "frame_bytes": flen, "median_us": round(med, 2),
+                              "p99_us": round(p99, 2), "calls": len(got),
+                              "cpu_restatement_median_us": round(zmed, 2)}), flush=True)
+        # a call after the wave has timed out (service relaunch included)
+        if service:
+            import time as _t
+            _t.sleep(0.01)
+            t0 = time.perf_counter()
+            eng.compute_one(frame)
+            print(json.dumps({"call": "compute_one after idle exit", "frame_bytes": flen,
+                              "us": round((time.perf_counter() - t0) * 1e6, 1)}), flush=True)
     for n in (16, 256, 4096):
         buf, offs, lens = synth.mixed_mtu_frames(n, seed=3)
         med, p99 = med_us(lambda: eng.compute_batch(buf, offs, lens), max(20, a.reps // 4))

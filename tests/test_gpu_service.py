@@ -1,0 +1,157 @@
+"""GPU: the per-packet service behind ricrc_compute_one (the latency form of
+the BTH.compute_icrc drop-in, src/roce.py:192-223): one resident wave polling
+a request slot in pinned host memory.  Every answer is checked against the
+oracle; the lifecycle (idle exit and relaunch, pause before batch work on the
+same context, destroy, process exit with the wave running) must never lose a
+request or leave a wave behind."""
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+import icrc_oracle as o  # noqa: E402  (checker only)
+from roce_icrc import IcrcEngine, synth  # noqa: E402
+
+
+def _frames():
+    """Frames of every shape compute_one sees: opcode shapes, 44 B .. 64 KiB,
+    IPv4 options, malformed ones (status bits, ICRC 0)."""
+    rng = np.random.default_rng(5)
+    out = [o.sim_send_success_frame()]
+    for pay in (0, 4, 60, 252, 1020, 4096, 9000, 65532 - 44):
+        out.append(o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x01, psn=pay, dqpn=3),
+                                 payload=rng.integers(0, 256, pay, dtype=np.uint8).tobytes()))
+    good = o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x0A, psn=1, dqpn=3),
+                         ext=o.reth_bytes(1, 2, 3), payload=bytes(100))
+    opt = bytearray(good[:20]) + b"\x01\x01\x01\x01" + good[20:]  # IPv4 options, IHL 6
+    opt[0] = 0x46
+    opt[2:4] = len(opt).to_bytes(2, "big")
+    out.append(bytes(opt))
+    bad = bytearray(out[1])
+    bad[0] = 0x65  # IP version 6
+    out.append(bytes(bad))
+    tcp = bytearray(out[2])
+    tcp[9] = 6  # not UDP
+    out.append(bytes(tcp))
+    out.append(out[3][:-2])  # length not a multiple of 4
+    return out
+
+
+def _want(f):
+    """The engine's contract: ICRC 0 (with a status bit) for what the
+    reference would not CRC, and for frames that are not a multiple of 4."""
+    if len(f) % 4 or o.masked_pseudo_packet(f) is None:
+        return 0
+    return o.icrc_of_frame(f)
+
+
+def test_service_answers_every_frame_shape(engine):
+    engine.set_service(1000)
+    for rep in range(3):
+        for f in _frames():
+            icrc, st = engine.compute_one(f)
+            assert icrc == _want(f), (len(f), hex(icrc), hex(_want(f)), st)
+            if len(f) % 4:
+                assert st & 0x01
+
+
+def test_service_many_calls_bit_exact(engine):
+    engine.set_service(1000)
+    buf, offs, lens = synth.mixed_mtu_frames(3000, seed=12)
+    for i in range(3000):
+        f = bytes(buf[int(offs[i]):int(offs[i] + lens[i])])
+        assert engine.compute_one(f)[0] == o.icrc_of_frame(f), i
+
+
+def test_service_idle_exit_and_relaunch(engine):
+    engine.set_service(2000)  # 2 ms idle timeout
+    f = o.sim_send_success_frame()
+    assert engine.compute_one(f)[0] == 0x1BE21D75
+    for gap in (0.0005, 0.005, 0.02, 0.0015, 0.0021):  # around and past the timeout
+        time.sleep(gap)
+        assert engine.compute_one(f)[0] == 0x1BE21D75, gap
+    engine.set_service(1000)
+
+
+def test_service_paused_by_batch_work_on_the_same_context(engine):
+    torch = pytest.importorskip("torch")
+    engine.set_service(1000)
+    n = 4096
+    buf, stride, flen = synth.uniform_frames(n, 4096, seed=3)
+    from conftest import oracle_batch
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    f = bytes(buf[:flen])
+    for _ in range(5):
+        assert engine.compute_one(f)[0] == want[0]
+        engine.compute_strided_dev(d, stride, flen, n, out)  # needs the CU the wave holds
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+        out.zero_()
+
+
+def test_batch_work_of_another_context_completes_beside_the_service(engine):
+    """A second context's full-grid launch while this context's wave holds one
+    CU: it completes (on the other CUs) and is bit-exact."""
+    torch = pytest.importorskip("torch")
+    engine.set_service(50000)  # keep the wave resident during the launches
+    f = o.sim_send_success_frame()
+    try:
+        assert engine.compute_one(f)[0] == 0x1BE21D75
+        n = 1 << 16
+        buf, stride, flen = synth.uniform_frames(n, 4096, seed=4)
+        from conftest import oracle_batch
+        want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+        with IcrcEngine(0) as other:
+            d = torch.from_numpy(buf).cuda()
+            out = torch.zeros(n, dtype=torch.int32, device="cuda")
+            for _ in range(3):
+                other.compute_strided_dev(d, stride, flen, n, out)
+                assert engine.compute_one(f)[0] == 0x1BE21D75
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    finally:
+        engine.set_service(1000)
+
+
+def test_service_off_is_the_launch_path(engine):
+    engine.set_service(0)
+    try:
+        for f in _frames()[:6]:
+            assert engine.compute_one(f)[0] == _want(f)
+    finally:
+        engine.set_service(1000)
+
+
+def test_destroy_with_the_wave_resident():
+    e = IcrcEngine(0)
+    e.set_service(100000)  # it would stay 100 ms without the stop
+    assert e.compute_one(o.sim_send_success_frame())[0] == 0x1BE21D75
+    t0 = time.perf_counter()
+    e.close()
+    assert time.perf_counter() - t0 < 0.05
+
+
+def test_process_exit_with_the_wave_resident():
+    """A process that ends without closing its engine: the library's exit
+    handler stops the wave before the runtime goes away."""
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "from roce_icrc import IcrcEngine\n"
+        "import icrc_oracle as o\n"
+        "e = IcrcEngine(0); e.set_service(1000000)\n"
+        "assert e.compute_one(o.sim_send_success_frame())[0] == 0x1BE21D75\n"
+        "print('answered', flush=True)\n"
+        % (str(ROOT / "roce-sim_amd"), str(ROOT / "oracle")))
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "answered" in r.stdout
+    assert time.perf_counter() - t0 < 60
