@@ -757,6 +757,15 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 // at (f, bk) owns [f, min(f + 16, cnt - bk)); a back claim owns
 // [max(cnt - bk - 8, f), cnt - bk): each side sees the other's position at
 // its own atomic, so the ranges are disjoint.
+//
+// Tiny frames (ACK / NAK / atomic-ack sized, <= kTinyLen bytes) are
+// instruction-bound even at G = 4: a G = 1 set (one lane per packet, 64
+// packets per wave) does a quarter of the per-packet work.  The sort gives
+// them a bucket of their own at the front of the window; when a window holds
+// at least kTinyMin of them, they run first as G = 1 sets ("phase A") with
+// Mul(128) staged into the G = 4 half of the Keys8 rows, and the G = 4 table
+// is restaged for the rest of the window (barriers around both restages; a
+// window of tiny frames only keeps Mul(128) for the next window).
 #ifndef RICRC_RAGGED_MIXED
 #define RICRC_RAGGED_MIXED 1
 #endif
@@ -766,6 +775,14 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 #define RICRC_MIXED_SHORT_LEN 600
 #endif
 constexpr uint32_t kMixedShortLen = RICRC_MIXED_SHORT_LEN;
+#ifndef RICRC_MIXED_TINY_LEN
+#define RICRC_MIXED_TINY_LEN 128
+#endif
+#ifndef RICRC_MIXED_TINY_MIN
+#define RICRC_MIXED_TINY_MIN 256
+#endif
+constexpr uint32_t kTinyLen = RICRC_MIXED_TINY_LEN;  // frames run as G = 1 sets (0: never)
+constexpr int kTinyMin = RICRC_MIXED_TINY_MIN;       // tiny frames a window needs for phase A
 // Ragged launches: workgroups per CU over the whole launch (one resident at a
 // time: the LDS holds one); more than one lets the dispatcher balance CUs.
 #ifndef RICRC_RAGGED_BLOCKS_PER_CU
@@ -827,8 +844,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   lds_u32* roff = (lds_u32*)(uintptr_t)LD::kRoff;
   lds_u16* rlen = (lds_u16*)(uintptr_t)LD::kRlen;
   constexpr uint32_t kNoOff = 0xFFFFFFFFu;
-  lds_u32* claim = (lds_u32*)(uintptr_t)(LD::kBase - 4u);  // (free word at the end of the LUT)
+  lds_u32* claim = (lds_u32*)(uintptr_t)(LD::kBase - 4u);  // (free words at the end of the LUT)
+  lds_u32* tclaim = (lds_u32*)(uintptr_t)(LD::kBase - 8u);  // phase A's claim counter
   const bool from_back = ((tid >> 6) & 1) != 0;
+  bool s_tiny = false;  // (uniform) the G = 4 half holds Mul(128) instead of Mul(512)
 
   const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
   const uint32_t wsz = p1 > p0 ? (p1 - p0 + nwin - 1) / nwin : 1;
@@ -836,6 +855,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     const int cnt = (int)min(wsz, p1 - w0);
     if (tid < NB) hist[tid] = 0;
     if (tid == NB) *claim = 0;
+    if (tid == NB + 1) *tclaim = 0;
     __syncthreads();
     constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
     int keys[KR];
@@ -863,13 +883,18 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
         if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
           const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
-          key = min(NB - 1, (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
+          // bucket 0: tiny frames (and unusable ones, which cost nothing)
+          key = L <= kTinyLen ? 0 : min(NB - 1, 1 + (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
         }
         atomicAdd((uint32_t*)&hist[key], 1u);
       }
       keys[r] = key;
     }
     __syncthreads();
+    // (uniform) the window's tiny frames, sorted to its front
+    const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
+    const int ntiny = ntiny_all >= kTinyMin ? ntiny_all : 0;
+    __syncthreads();  // every wave has read hist[0] before the scan rewrites it
     if (tid < 64) {  // exclusive scan of NB = 128 counts by one wave (2 per lane)
       const uint32_t c0 = hist[2 * tid], c1 = hist[2 * tid + 1];
       uint32_t s = c0 + c1;
@@ -900,12 +925,41 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       ob.ok_cap = (uint32_t)cnt;
       ob.ok_lds = LD::kOk;
     }
+    // ---- phase A: the tiny prefix [0, ntiny) as G = 1 sets of 64 packets,
+    // claimed from both ends, with Mul(128) in the Keys8 rows' G = 4 half
+    if (ntiny > 0) {
+      if (!s_tiny) {
+        MixedKeysS::template stage<kIcrcThreads>(a.tables + 0 * 1024, tid);  // main set 0: Mul(128)
+        s_tiny = true;
+        __syncthreads();
+      }
+      for (;;) {
+        uint32_t old = 0;
+        if (lane == 0) old = atomicAdd((uint32_t*)tclaim, from_back ? (64u << 16) : 64u);
+        old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+        const int f = (int)(old & 0xFFFFu), bk = (int)(old >> 16);
+        if (f + bk >= ntiny) break;
+        const int e = from_back ? ntiny - bk : min(f + 64, ntiny - bk);
+        const int s = from_back ? max(e - 64, f) : f;
+        mixed_set<0, VERIFY, MixedKeysS>(a, s, e, w0, lane, ob);
+      }
+      __syncthreads();  // phase A done before its table is replaced
+    }
+    if (ntiny < cnt && s_tiny) {  // (uniform) phase B needs Mul(512) back
+      MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
+      s_tiny = false;
+      __syncthreads();
+    }
+    // ---- phase B: [ntiny, cnt) as G = 4 / G = 8 sets (below), claims
+    // counted from ntiny
+    const int nb = cnt - ntiny;
     // Claim size: 16 packets while the frames at this wave's end of the window
     // are short, else 8.  Decided from the window's first 16 / last frame, then
     // from the wave's own previous claim (the front end only grows longer, the
     // back end only shorter), so a claim costs one LDS atomic.
-    uint32_t size = (uint32_t)__builtin_amdgcn_readfirstlane(
-                        (int)rlen[from_back ? cnt - 1 : min(15, cnt - 1)]) <= kMixedShortLen
+    uint32_t size = nb <= 0 ? 8u
+                    : (uint32_t)__builtin_amdgcn_readfirstlane(
+                          (int)rlen[from_back ? cnt - 1 : ntiny + min(15, nb - 1)]) <= kMixedShortLen
                         ? 16u : 8u;
 #ifdef RICRC_RAGGED_SORT_ONLY  // diagnostic build only: windows sorted, no set processed
     if (cnt < 0)
@@ -915,16 +969,16 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? (size << 16) : size);
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
       const int f = (int)(old & 0xFFFFu), bk = (int)(old >> 16);
-      if (f + bk >= cnt) break;
-      // the claim [s, e): 16 packets run as one G = 4 set if the longest
-      // (sorted last) is short, else as G = 8 sets of 8
+      if (f + bk >= nb) break;
+      // the claim [s, e) (window indices, from ntiny): 16 packets run as one
+      // G = 4 set if the longest (sorted last) is short, else as G = 8 sets of 8
       int s, e;
       if (from_back) {
         e = cnt - bk;
-        s = max(e - (int)size, f);
+        s = max(e - (int)size, ntiny + f);
       } else {
-        s = f;
-        e = min(f + (int)size, cnt - bk);
+        s = ntiny + f;
+        e = min(ntiny + f + (int)size, cnt - bk);
       }
       if (size == 16u) {
         const uint32_t longest = (uint32_t)__builtin_amdgcn_readfirstlane((int)rlen[e - 1]);
