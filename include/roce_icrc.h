@@ -298,6 +298,11 @@ int ricrc_stream_copy_dev(ricrc_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, 
  * loads, XOR-folded into d_sink[0]: the HBM-read denominator for the roofline. */
 int ricrc_stream_read_dev(ricrc_ctx* ctx, const uint8_t* d_buf, uint64_t bytes,
                           uint32_t* d_sink, void* stream);
+/* Timing of the last request the per-packet service answered: out3[0] / [1] =
+ * the GPU's 100 MHz real-time counter when the wave saw it / when its result
+ * was written (so (out3[1] - out3[0]) * 10 ns is the GPU-side time),
+ * out3[2] = the wave's polls of the request slot before it saw it. */
+int ricrc_ctx_service_times(ricrc_ctx* ctx, uint64_t* out3);
 /* Lanes per packet the engine would use for frames of `len` bytes (1 for the
  * lane-per-packet kernel of small strided frames). */
 int ricrc_lanes_for_len(ricrc_ctx* ctx, uint32_t len);

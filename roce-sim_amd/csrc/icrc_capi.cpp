@@ -454,7 +454,7 @@ int service_ensure(ricrc_ctx* c) {
   ricrc::ServiceArgs a{};
   a.ring = r;  // (unified addressing: the mapped host pointer is the device pointer)
   a.tables = c->d_tables;
-  a.served = __atomic_load_n(&r->req_seq, __ATOMIC_ACQUIRE);
+  a.served = (uint32_t)__atomic_load_n(&r->req, __ATOMIC_ACQUIRE);
   a.idle_ticks = (uint64_t)c->svc_idle_us * 100u;  // 100 MHz real-time counter
   std::atomic_thread_fence(std::memory_order_seq_cst);
   HIP_TRY(ricrc::launch_service(a, c->svc_stream));
@@ -473,18 +473,21 @@ int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icr
   if (rc) return rc;
   ricrc::ServiceRing* r = c->svc;
   std::memcpy((uint8_t*)r + ricrc::kSvcFrame, frame, len);
-  r->len = len;
   const uint32_t seq = ++c->svc_seq == 0 ? ++c->svc_seq : c->svc_seq;  // (0 = nothing yet)
-  __atomic_store_n(&r->req_seq, seq, __ATOMIC_RELEASE);
+  __atomic_store_n(&r->req, ((uint64_t)len << 32) | seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
+  uint64_t ans = 0;
+  auto answered = [&] {
+    ans = __atomic_load_n(&r->resp, __ATOMIC_ACQUIRE);
+    return (uint32_t)(ans >> 40) == (seq & ricrc::kSvcSeqMask);
+  };
   for (uint32_t spin = 1;; ++spin) {
-    if (__atomic_load_n(&r->resp_seq, __ATOMIC_ACQUIRE) == seq) break;
+    if (answered()) break;
     if ((spin & 255u) == 0) {
       // the wave may have left (idle timeout) just before the request was
       // published: once its stream is idle and the answer is still missing,
       // launch it again (it serves the pending request first)
-      if (hipStreamQuery(c->svc_stream) == hipSuccess &&
-          __atomic_load_n(&r->resp_seq, __ATOMIC_ACQUIRE) != seq) {
+      if (hipStreamQuery(c->svc_stream) == hipSuccess && !answered()) {
         c->svc_launched = false;
         rc = service_ensure(c);
         if (rc) return rc;
@@ -496,8 +499,8 @@ int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icr
     }
     __builtin_ia32_pause();
   }
-  *icrc_out = r->icrc;
-  if (status_out) *status_out = (uint8_t)r->status;
+  *icrc_out = (uint32_t)ans;
+  if (status_out) *status_out = (uint8_t)(ans >> 32);
   return RICRC_OK;
 }
 
@@ -605,6 +608,18 @@ int ricrc_ctx_set_service(ricrc_ctx* c, uint32_t idle_us) {
   if (idle_us == 0 && c->svc) service_stop_wait(c);
   c->svc_idle_us = idle_us;
   if (c->svc_launched) service_pause(c);  // the next call relaunches with the new timeout
+  return RICRC_OK;
+}
+
+int ricrc_ctx_service_times(ricrc_ctx* c, uint64_t* out3) {
+  if (!c || !out3) return RICRC_EINVAL;
+  if (!c->svc) {
+    out3[0] = out3[1] = out3[2] = 0;
+    return RICRC_OK;
+  }
+  out3[0] = c->svc->t_seen;
+  out3[1] = c->svc->t_done;
+  out3[2] = c->svc->polls;
   return RICRC_OK;
 }
 

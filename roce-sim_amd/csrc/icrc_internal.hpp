@@ -96,16 +96,24 @@ namespace ricrc {
 // response slot in pinned fine-grained host memory.  Host-written words and
 // GPU-written words sit on separate 128-byte lines; the frame at kSvcFrame.
 struct ServiceRing {
-  uint32_t req_seq;  // host: published (release) after len and the frame
-  uint32_t len;      // host: frame bytes incl. the ICRC slot
-  uint32_t stop;     // host: 1 = leave now
+  // host: sequence number (low 32 bits) and frame length incl. the ICRC slot
+  // (high 32), published with ONE 8-byte release store after the frame, so
+  // the wave learns both with one PCIe read and issues the frame's loads at
+  // once (a separate length word cost a second round trip, ~1.5 us)
+  uint64_t req;
+  uint32_t stop;  // host: 1 = leave now
   uint32_t pad0[29];
-  uint32_t resp_seq;  // GPU: = req_seq once icrc / status hold its result
-  uint32_t icrc;
-  uint32_t status;
+  // GPU: the answer, ONE 8-byte store: ICRC (bits 0-31), status (32-39) and
+  // the request's sequence number mod 2^24 (40-63) -- no fence between a
+  // result and its sequence number
+  uint64_t resp;
   uint32_t exited;  // GPU: 1 when the wave has left its loop
-  uint32_t pad1[28];
+  uint32_t polls;   //      poll iterations before the last request was seen
+  uint64_t t_seen;  //      real-time counter (100 MHz) when it was seen
+  uint64_t t_done;  //      ... when its result was ready
+  uint32_t pad1[24];
 };
+constexpr uint32_t kSvcSeqMask = 0xFFFFFFu;
 constexpr uint32_t kSvcFrame = 1024;  // frame offset in the slot (aligned grid: 1 KiB at G = 64)
 constexpr uint32_t kSvcMaxFrame = 65536;
 constexpr size_t kSvcBytes = kSvcFrame + kSvcMaxFrame;

@@ -1356,8 +1356,9 @@ __global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4
 //
 // Polling uses relaxed system-scope loads (no cache maintenance per poll);
 // one acquire fence per request makes the frame bytes the host wrote before
-// publishing visible, one release fence publishes the result before the
-// sequence number.  The wave leaves when the host raises `stop` (context
+// publishing visible.  The request (sequence number + length) and the answer
+// (ICRC + status + sequence number) are single 8-byte words, so each
+// direction is one PCIe transaction with no fence between value and flag.  The wave leaves when the host raises `stop` (context
 // destroyed, or about to launch batch work, which needs this CU's LDS) or
 // after `idle_ticks` of the 100 MHz real-time counter without a request:
 // every path through the loop reaches one of the two, so the grid always
@@ -1374,25 +1375,43 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   const MainKeys kk = MainKeys::make(lane);
   ServiceRing* r = s.ring;
   const uint8_t* frame = (const uint8_t*)r + kSvcFrame;
+  // the group's result goes to two LDS words past the tables (flat stores
+  // through generic pointers), then out as one 8-byte answer
+  constexpr uint32_t kOut = (uint32_t)kFixLut<6, MainKeys> + 256u - 16u;  // (the LUT's spare bytes)
   IcrcArgs a{};
   a.frames = frame;
   a.n = 1;
-  a.icrc_out = &r->icrc;
-  a.status_out = (uint8_t*)&r->status;  // (the low byte of the word, little-endian)
+  a.icrc_out = (uint32_t*)(lds_u32*)(uintptr_t)kOut;
+  a.status_out = (uint8_t*)(lds_u32*)(uintptr_t)(kOut + 4u);
   uint32_t served = s.served;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)__hip_atomic_load(&r->req_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  uint32_t polls = 0;
+  for (;; ++polls) {
+    const uint64_t req = __hip_atomic_load(&r->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)req);
     if (seq != served) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before seq
-      const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)__hip_atomic_load(&r->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before req
+      const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(req >> 32));
       const Pkt p = describe<DPI>(frame, 0, true, 0, L <= kSvcMaxFrame ? L : 0u);
       Batch<kUnroll> b = issue_packet<LOG2G, false>(p, lane);
       finish_packet<LOG2G, false>(a, p, b, lane, 0, kk);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // icrc / status before the sequence number
-      if (lane == 0) __hip_atomic_store(&r->resp_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // the flat stores of the result (through generic pointers into LDS)
+      // have landed before lane 0 reads the words back with LDS reads
+      __asm__ __volatile__("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0);
+      __asm__ __volatile__("" ::: "memory");
+      if (lane == 0) {
+        const uint64_t ans = (uint64_t)lds_rd(kOut) | ((uint64_t)(lds_rd(kOut + 4u) & 0xFFu) << 32) |
+                             ((uint64_t)(seq & kSvcSeqMask) << 40);
+        // (timing of this request for ricrc_ctx_service_times: diagnostics,
+        // not ordered against the answer)
+        r->t_seen = t_seen;
+        r->t_done = __builtin_amdgcn_s_memrealtime();
+        r->polls = polls;
+        __hip_atomic_store(&r->resp, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      polls = 0;
       served = seq;
       t_last = __builtin_amdgcn_s_memrealtime();
       continue;

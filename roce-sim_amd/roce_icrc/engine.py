@@ -80,6 +80,7 @@ _SIGNATURES = {
     "ricrc_ctx_set_lanes_per_packet": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ricrc_ctx_stream": (_vp, [_vp]),
     "ricrc_ctx_set_service": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "ricrc_ctx_service_times": (ctypes.c_int, [_vp, _vp]),
     "ricrc_compute_one": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, _vp]),
     "ricrc_compute_batch": (
         ctypes.c_int,
@@ -283,6 +284,13 @@ class IcrcEngine:
         """Idle timeout of the per-packet service behind compute_one (0 = off:
         one kernel launch per call)."""
         self._check("ricrc_ctx_set_service", self.lib.ricrc_ctx_set_service(self.ctx, idle_us))
+
+    def service_times(self) -> tuple[float, int]:
+        """(GPU-side microseconds, polls) of the last request the per-packet
+        service answered."""
+        t = np.zeros(3, np.uint64)
+        self._check("ricrc_ctx_service_times", self.lib.ricrc_ctx_service_times(self.ctx, _ptr(t)))
+        return float(int(t[1]) - int(t[0])) * 0.01, int(t[2])
 
     def lanes_for_len(self, length: int) -> int:
         return self.lib.ricrc_lanes_for_len(self.ctx, length)

@@ -47,9 +47,17 @@ def main():
             # the reference's own arithmetic on this host, per frame (zlib.crc32
             # of the masked pseudo packet, src/roce.py:218), for scale
             zmed, _ = med_us(lambda: orc.icrc_of_frame(frame), a.reps)
+            gpu = []
+            if service:  # GPU-side share of a call (wave saw it -> result written)
+                for _ in range(50):
+                    eng.compute_one(frame)
+                    gpu.append(eng.service_times())
             print(json.dumps({"call": "compute_one", "service_idle_us": service,
                               "frame_bytes": flen, "median_us": round(med, 2),
                               "p99_us": round(p99, 2), "calls": len(got),
+                              "gpu_side_median_us": round(float(np.median([g[0] for g in gpu])), 2)
+                              if gpu else None,
+                              "polls_median": float(np.median([g[1] for g in gpu])) if gpu else None,
                               "cpu_restatement_median_us": round(zmed, 2)}), flush=True)
         # a call after the wave has timed out (service relaunch included)
         if service:
