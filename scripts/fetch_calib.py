@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--layout", default="packed", choices=("packed", "spaced"))
     ap.add_argument("--packets", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--time", type=int, default=0, help="also time this many launches")
     a = ap.parse_args()
     eng = IcrcEngine(0)
     dev = torch.device("cuda", 0)
@@ -106,7 +107,18 @@ def main():
     for _ in range(a.reps):
         step()
     torch.cuda.synchronize()
+    ms = None
+    if a.time:  # (not under the profiler) HIP-event median over `time` launches
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.time)]
+        for e0, e1 in ev:
+            e0.record()
+            step()
+            e1.record()
+        torch.cuda.synchronize()
+        ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
     print(json.dumps({"workload": a.workload, "layout": a.layout, "packets": n, "reps": a.reps,
+                      "kernel_ms_median": ms,
                       "frame_line_bytes": line_bytes, "descriptor_bytes": desc_bytes,
                       "known_read_bytes": None if line_bytes is None else line_bytes + desc_bytes,
                       "output_bytes": out_bytes}), flush=True)

@@ -42,8 +42,15 @@ else
   BUF=$(python3 -c "import json; d=json.load(open('$OUT/bench_$TAG.json')); c=d['config']; print((c['covered_bytes_per_gpu'] + 4 * c['packets_per_gpu']) // 16 * 16)")
   KN=::icrc_
   [ "$WL" = cfg3 ] && KN="true>(ricrc::IcrcArgs"  # the verify kernel, either ragged form (the compute launch in setup fills trailers)
+  # FETCH_SIZE factor measured on this workload's own access pattern (scripts/fetch_calib.py)
+  CAL=""
+  CF=$R/profiles/r03b_fetch_calibration/$WL.json
+  if [ -f $CF ]; then
+    F=$(python3 -c "import json; print(json.load(open('$CF'))['factor'])")
+    CAL="--calibration $F --calibration-source profiles/r03b_fetch_calibration/$WL.json"
+  fi
   python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
-    --packets $NP --frame-bytes 0 --ceiling-read-bytes $BUF --alg-bytes $ALG --kernel "$KN" \
+    --packets $NP --frame-bytes 0 --ceiling-read-bytes $BUF --alg-bytes $ALG --kernel "$KN" $CAL \
     --out $OUT/pmc_traffic_${TAG}_$WL.json || exit 1
 fi
 python3 scripts/prof_summary.py $OUT/prof_$TAG $OUT/bench_$TAG.json "$KN" > $OUT/prof_summary_$TAG.txt || exit 1
