@@ -24,10 +24,13 @@
  * (src/roce.py:204), so callers pass the bytes exactly as they go on the wire.
  *
  * Per-packet status.  A frame that is not IPv4 (version != 4 or IHL < 5), not
- * UDP (protocol != 17), shorter than IP+UDP+BTH+ICRC, longer than 65535 bytes
- * or not a multiple of 4 bytes long gets ICRC 0 and a status bit -- the
- * reference's "warning + ICRC 00000000" path (src/roce.py:195-200, 220-223).
- * These are not call errors: the batch call still returns RICRC_OK.
+ * UDP (protocol != 17), shorter than IP+UDP+BTH+ICRC or longer than 65535
+ * bytes gets ICRC 0 and a status bit -- the reference's "warning + ICRC
+ * 00000000" path (src/roce.py:195-200, 220-223).  These are not call errors:
+ * the batch call still returns RICRC_OK.  Frames of any other length are
+ * CRC'd like zlib.crc32 does (those that are not a multiple of 4 bytes long,
+ * which roce-sim's emit paths never build, and those at unaligned addresses
+ * take a slower byte-load path).
  *
  * Ownership.  The caller owns every buffer.  No pointer is retained after a
  * synchronous call returns; the *_dev variants are asynchronous on `stream`
@@ -60,7 +63,7 @@ extern "C" {
 #define RICRC_EIO (-5)     /* HIP runtime or kernel launch failure          */
 
 /* per-packet status bits (status_out[i]) */
-#define RICRC_PKT_BAD_LEN 0x01       /* len % 4, too short, or > 65535 */
+#define RICRC_PKT_BAD_LEN 0x01       /* too short, or > 65535                     */
 #define RICRC_PKT_NOT_IPV4 0x02      /* IP version != 4 or IHL < 5 (ICRC = 0)     */
 #define RICRC_PKT_NOT_UDP 0x04       /* IP protocol != 17 (ICRC = 0)              */
 #define RICRC_PKT_LEN_MISMATCH 0x08  /* IP total length != len (ICRC still computed) */

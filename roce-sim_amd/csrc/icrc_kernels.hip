@@ -102,12 +102,15 @@ __device__ __forceinline__ Pkt describe(const uint8_t* frames, uint32_t pkt, boo
   p.L = L;
   p.pkt = pkt;
   p.live = live;
-  const bool lenbad = L < 44 || (L & 3u) || L > 65535u;
-  p.unal = live && !lenbad && ((uintptr_t)p.fp & 3u) != 0;
+  const bool lenbad = L < 44 || L > 65535u;
+  // a frame at an unaligned start, or whose length is not a multiple of 4
+  // (the reference CRCs any length; none of its own emit paths builds one),
+  // takes the byte-load slow path
+  p.unal = live && !lenbad && (((uintptr_t)p.fp & 3u) != 0 || (L & 3u) != 0);
   p.dead = !live || lenbad || (p.unal && !unal_ok);
   p.S = p.unal ? 0 : (int)(((uintptr_t)p.fp >> 2) & (DPI - 1));
   p.ab = p.fp - 4 * p.S;
-  p.n = p.dead ? 1 : (int)((L - 4) >> 2);
+  p.n = p.dead ? 1 : (int)((L - 4 + 3) >> 2);  // covered dwords, the last maybe partial
   const int E = p.S + p.n;
   p.J = (E + DPI - 1) / DPI;
   p.r = E - DPI * (p.J - 1);
@@ -145,20 +148,41 @@ __device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
   return v;
 }
 
-// The slow path's chunk of a frame at an unaligned start: byte loads of the
-// covered dwords only (nothing outside the frame is touched).
+// The slow path's chunk of a frame at an unaligned start or of a length that
+// is not a multiple of 4: byte loads of the covered dwords only (nothing
+// outside the frame is touched).  The last covered dword of such a length
+// holds 1-3 covered bytes; its other bytes (the ICRC slot's) enter as zeros,
+// i.e. the frame is CRC'd as if followed by 4 - L % 4 zero bytes, which
+// slow_packet takes back out of the register (unshift_zero_bytes).
 __device__ __forceinline__ uint32_t ldg32_bytes(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 template <int G>
 __device__ __forceinline__ u32x4 load_chunk_bytes(const Pkt& p, int j, int gl) {
   const int kb = 4 * G * j + 4 * gl - p.S;
+  const uint32_t m = p.L & 3u;
+  const uint32_t keep = m ? (1u << (8u * m)) - 1u : 0xFFFFFFFFu;  // of the last dword
   u32x4 v = {0, 0, 0, 0};
-  if (kb + 0 >= 0 && kb + 0 < p.n) v.x = ldg32_bytes(p.fp + 4 * (kb + 0));
-  if (kb + 1 >= 0 && kb + 1 < p.n) v.y = ldg32_bytes(p.fp + 4 * (kb + 1));
-  if (kb + 2 >= 0 && kb + 2 < p.n) v.z = ldg32_bytes(p.fp + 4 * (kb + 2));
-  if (kb + 3 >= 0 && kb + 3 < p.n) v.w = ldg32_bytes(p.fp + 4 * (kb + 3));
+#define RICRC_BYTES(c, t)                                                            \
+  if (kb + (t) >= 0 && kb + (t) < p.n) {                                             \
+    v.c = ldg32_bytes(p.fp + 4 * (kb + (t)));                                        \
+    if (kb + (t) == p.n - 1) v.c &= keep;                                            \
+  }
+  RICRC_BYTES(x, 0)
+  RICRC_BYTES(y, 1)
+  RICRC_BYTES(z, 2)
+  RICRC_BYTES(w, 3)
+#undef RICRC_BYTES
   return v;
+}
+
+// The reflected CRC register with `z` zero bytes taken back off its end:
+// multiplication by x^(-8 z) mod P, one inverse register step per bit (the
+// forward step is r -> (r >> 1) ^ (r & 1 ? P : 0), and P has bit 31 set).
+__device__ __forceinline__ uint32_t unshift_zero_bytes(uint32_t r, uint32_t z) {
+  for (uint32_t b = 0; b < 8u * z; ++b)
+    r = (r & 0x80000000u) ? (((r ^ kPoly) << 1) | 1u) : (r << 1);
+  return r;
 }
 
 // Body iterations (jh <= j < J-1) lie wholly inside the frame: no predicate.
@@ -228,8 +252,9 @@ __device__ __noinline__ uint32_t slow_packet(Pkt p, int ihl, int gl, int base) {
     else
       fold(A, w, kk);
   }
-  return combine<LOG2G, K>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2], A.P[3] ^ A.T[3],
-                           p.r, gl, base);
+  const uint32_t B = combine<LOG2G, K>(A.P[0] ^ A.T[0], A.P[1] ^ A.T[1], A.P[2] ^ A.T[2],
+                                       A.P[3] ^ A.T[3], p.r, gl, base);
+  return (p.L & 3u) ? unshift_zero_bytes(B, 4u - (p.L & 3u)) : B;
 }
 
 
@@ -1077,6 +1102,32 @@ constexpr int kSmallOutRounds = RICRC_SMALL_OUTBUF;  // output ring depth in rou
 #endif
 constexpr int kSmallOutPol = RICRC_SMALL_OUT_POL;
 
+// The four-chain fold of the small kernel over dwords [0, n) of one frame,
+// each dword through the per-dword masks of an IHL of `ihl` (IPv4 options,
+// malformed frames, the last batch read straight from global memory: frame at
+// `f`; else the frame staged in LDS at `pb`).  Out of line: its per-dword
+// mask constants are uniform values the hot loop would otherwise keep live
+// (they were ~200 SGPRs spilled to VGPR lanes in round 2, all in this path).
+template <bool GLOBAL>
+__device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb, int ihl, int n) {
+  const SmallKeys kk = SmallKeys::make(__lane_id());
+  const int ns = (n + 3) >> 2, pad = 4 * ns - n;
+  uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+  for (int j = 0; j < ns; ++j) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = 4 * j + c - pad;
+      uint32_t w = 0;
+      if (k >= 0) w = fix_dword(GLOBAL ? ldg32(f + 4 * k) : lds_rd(pb + 4u * (uint32_t)k), k,
+                                ihl + 1, ihl + 3);
+      kk.absorb(P[c], T[c], w);
+    }
+  }
+  uint32_t R = mul_comb(P[3] ^ T[3], kSmallComb) ^ P[2] ^ T[2];
+  R = mul_comb(R, kSmallComb) ^ P[1] ^ T[1];
+  return mul_comb(R, kSmallComb) ^ P[0] ^ T[0];
+}
+
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
@@ -1174,9 +1225,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     return mul_comb(R, kSmallComb) ^ P[0] ^ T[0];
   };
   // per-dword masks (IPv4 options, the direct path, malformed frames)
-  auto fold4_masked = [&](int ihl, auto src) {
-    return fold4([&](int k, int) { return fix_dword(src(k), k, ihl + 1, ihl + 3); });
-  };
+
   // Batches a wave loads are clamped to the workgroup's own staged range:
   // the prefetch two rounds past its end re-reads the range's last batch
   // (still in L2) instead of the next workgroup's first ones, which that
@@ -1235,7 +1284,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       R = fold4([&](int, int kp) { return lds_rd(pz + 4u * (uint32_t)kp); });
 #endif
     } else {
-      R = fold4_masked(ihl, [&](int k) { return lds_rd(pb + 4u * (uint32_t)k); });
+      R = small_fold_masked<false>(nullptr, pb, ihl, n);
     }
     emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing);
     __asm__ __volatile__("" ::: "memory");
@@ -1307,7 +1356,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
     int ihl;
     const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
-    const uint32_t R = fold4_masked(ihl, [&](int k) { return ldg32(f + 4 * k); });
+    const uint32_t R = small_fold_masked<true>(f, 0u, ihl, n);
     emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
   }
 }

@@ -356,9 +356,6 @@ class BTH(Packet):
             return self.pack_icrc(0)
         frame = wire_frame(ip, udp, p)
         icrc, status = get_engine().compute_one(frame)
-        if status & PKT_BAD_LEN:  # see emit_batch: no engine ICRC for such a frame
-            raise ValueError(f"BTH.compute_icrc: the {len(frame)}-byte frame is not a multiple of "
-                             "4 bytes long (pad the payload: add_padding_if_needed / l3_packet)")
         return self.pack_icrc(icrc ^ self.icrc_fault)
 
     def build_payload(self):
@@ -537,11 +534,10 @@ def emit_batch(pkts: list[Packet]) -> list[bytes]:
     ``icrc`` keep it; the UDP checksum is recomputed over the final trailer.
 
     Per-packet status as ``BTH.compute_icrc`` (src/roce.py:195-200, 220-223):
-    a frame that is not IPv4/UDP gets ICRC 0 with a warning.  A frame whose
-    length is not a multiple of 4 raises ValueError: the engine CRCs dword
-    multiples only (every frame the reference's emit paths build is one:
-    ``send_ip_pkt`` / ``send_pkt`` pad the payload, src/roce_util.py:187-199),
-    and writing the engine's 0 for it would not be the reference's ICRC."""
+    a frame that is not IPv4/UDP gets ICRC 0 with a warning.  Any length is
+    CRC'd, as ``zlib.crc32`` does (one that is not a multiple of 4, which the
+    reference's padded emit paths never build, takes the engine's byte-load
+    path)."""
     frames, need = [], []
     for i, pkt in enumerate(pkts):
         bth = pkt.getlayer(BTH)
@@ -556,13 +552,8 @@ def emit_batch(pkts: list[Packet]) -> list[bytes]:
         # frames at dword-aligned offsets, whatever their lengths
         buf, offs, lens = pack_aligned([frames[i] for i in need])
         icrc, st = get_engine().compute_batch(buf, offs, lens)
-        bad = [need[j] for j in np.flatnonzero(st & PKT_BAD_LEN)]
-        if bad:
-            raise ValueError(f"emit_batch: frames {bad[:8]} are {[len(frames[i]) for i in bad[:8]]} "
-                             "bytes long; the ICRC engine takes frames of a multiple of 4 bytes "
-                             "(pad the payload: add_padding_if_needed / l3_packet)")
-        for j in np.flatnonzero(st & (PKT_NOT_IPV4 | PKT_NOT_UDP)):
-            warnings.warn(f"emit_batch: frame {need[j]} is not IPv4/UDP: ICRC 0 "
+        for j in np.flatnonzero(st & (PKT_BAD_LEN | PKT_NOT_IPV4 | PKT_NOT_UDP)):
+            warnings.warn(f"emit_batch: frame {need[j]} is not a CRC-able IPv4/UDP frame: ICRC 0 "
                           "(BTH.compute_icrc's warning path, src/roce.py:195-200, 220-223)")
         for j, i in enumerate(need):
             f = bytearray(frames[i])

@@ -88,9 +88,9 @@ def test_odd_length_datagram_does_not_shift_the_batch(engine):
     """A stray datagram whose length is not a multiple of 4 (truncated UDP
     packet) in the middle of a receive batch: it fails, and every valid frame
     after it still verifies and is delivered (frames are packed at dword-aligned
-    offsets).  On the emit side an odd-length frame is refused with ValueError
-    instead of getting the engine's ICRC 0 (the reference would CRC it; its
-    own emit paths always pad, src/roce_util.py:187-199)."""
+    offsets).  On the emit side an odd-length frame gets the reference's ICRC
+    (zlib.crc32 takes any length; the engine's byte-load path), and the
+    frames after it theirs."""
     R.set_engine(engine)
     pkts = [R.l3_packet(R.BTH(opcode=0x01, psn=i, dqpn=0x30) / R.Raw(load=bytes([i]) * 64),
                         dst="10.0.0.2", sport=7, src="10.0.0.1") for i in range(8)]
@@ -105,8 +105,10 @@ def test_odd_length_datagram_does_not_shift_the_batch(engine):
     # emit side: a BTH/Raw build without padding gives an odd-length frame
     raw = R.IP(src="10.0.0.1", dst="10.0.0.2") / R.UDP(dport=4791, sport=7) / \
         R.BTH(opcode=0x04, psn=99, dqpn=0x30) / R.Raw(load=b"\x01\x02\x03")
-    with pytest.raises(ValueError, match="multiple of 4"):
-        R.emit_batch(pkts[:2] + [raw] + pkts[2:])
+    mixed = R.emit_batch(pkts[:2] + [raw] + pkts[2:])
+    assert len(mixed[2]) % 4 == 3 and mixed[:2] + mixed[3:] == frames
+    assert mixed[2][-4:] == int(o.icrc_of_frame(mixed[2])).to_bytes(4, "little")
+    assert o.verify_frame(mixed[2]) and R.verify_frames([mixed[2]])[0]
     # padded as the reference's emit wrap pads it, the same packet goes through
     padded = R.l3_packet(R.BTH(opcode=0x04, psn=99, dqpn=0x30) / R.Raw(load=b"\x01\x02\x03"),
                          dst="10.0.0.2", sport=7, src="10.0.0.1")

@@ -177,7 +177,7 @@ def test_edge_cases_and_status(engine):
     not_ip = b"\x60" + good[1:]          # IPv6 version nibble
     not_udp = good[:9] + b"\x06" + good[10:]  # TCP protocol
     short = good[:40]                    # shorter than IP+UDP+BTH+ICRC
-    odd = good + b"\0\0"                 # length not a multiple of 4
+    odd = good + b"\0\0"                 # length not a multiple of 4 (CRC'd, as zlib would)
     mism = good[:2] + b"\x00\x10" + good[4:]  # IP total length != frame length
     # IPv4 with options (IHL 6): masks move with the UDP/BTH offsets
     opt = bytearray(good[:20]) + b"\x01\x01\x01\x01" + good[20:]
@@ -192,7 +192,7 @@ def test_edge_cases_and_status(engine):
     assert got[2] == 0 and st[2] & PKT_NOT_IPV4
     assert got[3] == 0 and st[3] & PKT_NOT_UDP
     assert got[4] == 0 and st[4] & PKT_BAD_LEN
-    assert got[5] == 0 and st[5] & PKT_BAD_LEN
+    assert got[5] == o.icrc_of_frame(odd) != 0 and st[5] == PKT_LEN_MISMATCH
     assert got[6] == o.icrc_of_frame(mism) and st[6] == PKT_LEN_MISMATCH
     assert got[7] == o.icrc_of_frame(opt) and st[7] == 0
     # empty batch and single frame at the very end of the buffer
@@ -560,7 +560,8 @@ def test_ragged_many_windows_random_sizes(engine):
     so every workgroup sorts several windows -- two of 6144 in the
     mixed-width kernel, whose windows hold up to 8192 -- and claims sets from
     both ends of each), laid out in memory order with malformed frames
-    scattered in: lengths not a multiple of 4, TCP instead of UDP, an IP total
+    scattered in: lengths not a multiple of 4 (CRC'd through the byte-load
+    path, as zlib.crc32 would), TCP instead of UDP, an IP total
     length that disagrees with the frame, IPv4 options.  Lane settings 4, 8
     (the mixed-width kernel: G = 4 and G = 8 sets) and 16; compute and verify
     against the C oracle."""
@@ -585,20 +586,17 @@ def test_ragged_many_windows_random_sizes(engine):
     buf[o64[opt]] = 0x46
     odd = rng.choice(n, 500, replace=False)
     lens_k = lens.copy()
-    lens_k[odd] -= 2  # ends 2 bytes early: not a multiple of 4
+    lens_k[odd] -= (2 + 4 * (odd % 3)).astype(np.uint32)  # 2 / 6 / 10 bytes early: not a multiple of 4
     want, _ = oracle_batch(buf, offsets=offs, lens=lens)
-    good = np.ones(n, bool)
-    good[odd] = False
     # trailers = the oracle's words (frames it rejects keep 0 there, and so
     # fail verification like on the GPU); then one payload bit of every 1013th
     trail = o64 + lens.astype(np.int64) - 4
     buf[(trail[:, None] + np.arange(4)[None, :]).reshape(-1)] = want.view(np.uint8)
     flip = np.arange(5, n, 1013)
     buf[o64[flip] + 40] ^= 0x08
-    want, ok_want = oracle_batch(buf, offsets=offs, lens=lens)
-    fatal = np.zeros(n, bool)
-    fatal[tcp] = True
-    fatal[odd] = True
+    # the oracle over the lengths the GPU is given (odd ones included: any
+    # length is CRC'd, as zlib.crc32 does; their trailers do not match)
+    want, ok_want = oracle_batch(buf, offsets=offs, lens=lens_k)
     d = torch.from_numpy(buf).cuda()
     do = torch.from_numpy(offs.view(np.int64)).cuda()
     dl = torch.from_numpy(lens_k.view(np.int32)).cuda()
@@ -615,10 +613,9 @@ def test_ragged_many_windows_random_sizes(engine):
             engine.set_lanes(0)
         got = out.cpu().numpy().view(np.uint32)
         okh = ok.cpu().numpy().astype(bool)
-        np.testing.assert_array_equal(got[good], want[good], err_msg=f"lanes {lanes}")
-        assert (got[odd] == 0).all()
-        exp_ok = ok_want.astype(bool) & ~fatal
-        np.testing.assert_array_equal(okh, exp_ok, err_msg=f"lanes {lanes}")
+        np.testing.assert_array_equal(got, want, err_msg=f"lanes {lanes}")
+        assert not okh[odd].any()  # (their trailers do not match)
+        np.testing.assert_array_equal(okh, ok_want.astype(bool), err_msg=f"lanes {lanes}")
         assert not okh[flip].any() and okh.sum() > n - 5000
 
 
@@ -770,3 +767,76 @@ def test_small_kernel_beyond_4_gib(engine):
     assert bad.size == 0, f"tiles with wrong words: {bad.tolist()}"
     del d
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("lanes", [0, 1, 4, 8, 64])
+def test_any_frame_length(engine, lanes):
+    """zlib.crc32 takes any length, so does the reference's compute_icrc: frames
+    of every length 44 .. 700 B (every residue mod 4) at every byte alignment,
+    ragged (host and device) and strided with odd strides, compute and verify
+    (trailers = the oracle's words, every 7th with a flipped covered bit)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(4242 + lanes)
+    frames = []
+    for L in range(44, 701):
+        f = bytearray(o.build_frame("10.1.2.3", "10.3.2.1", 77, dict(opcode=0x07, psn=L),
+                                    payload=rng.integers(0, 256, L - 44, dtype=np.uint8).tobytes()))
+        del f[L:]  # the exact length (a payload of L - 44 bytes was padded to 4)
+        f[2:4] = L.to_bytes(2, "big")
+        frames.append(bytes(f))
+    offs, pos = [], 0
+    for i, f in enumerate(frames):
+        pos += i % 4  # every byte misalignment in turn
+        offs.append(pos)
+        pos += len(f)
+    buf = np.zeros(pos + 8, np.uint8)
+    for off, f in zip(offs, frames):
+        buf[off:off + len(f)] = np.frombuffer(f, np.uint8)
+    offs = np.array(offs, np.uint64)
+    lens = np.array([len(f) for f in frames], np.uint32)
+    want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
+    for i, (a, L) in enumerate(zip(offs, lens)):
+        e = int(a + L)
+        buf[e - 4:e] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    flip = np.arange(3, len(frames), 7)
+    for i in flip:
+        buf[int(offs[i]) + 42] ^= 0x10
+    want, ok_want = oracle_batch(buf, offs, lens)
+    assert (want != 0).all()
+    engine.set_lanes(lanes)
+    try:
+        got, st = engine.compute_batch(buf, offs, lens)
+        ok, got2, _ = engine.verify_batch(buf, offs, lens)
+        d = torch.from_numpy(buf).cuda()
+        do = torch.from_numpy(offs.view(np.int64)).cuda()
+        dl = torch.from_numpy(lens.view(np.int32)).cuda()
+        dout = torch.zeros(len(frames), dtype=torch.int32, device="cuda")
+        engine.compute_batch_dev(d, do, dl, len(frames), dout)
+        torch.cuda.synchronize()
+    finally:
+        engine.set_lanes(0)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got2, want)
+    np.testing.assert_array_equal(dout.cpu().numpy().view(np.uint32), want)
+    np.testing.assert_array_equal(ok, ok_want.astype(bool))
+    assert not ok[flip].any() and ok.sum() == len(frames) - flip.size
+    assert not (st & PKT_BAD_LEN).any()
+    # strided, every length residue and odd strides (the small-frame kernel
+    # takes multiples of 4 only; the rest go through the lane-group kernels)
+    for L, stride in ((45, 45), (46, 47), (47, 48), (101, 101), (4139, 4141)):
+        n = 1001
+        fr = bytearray(o.build_frame("10.1.2.3", "10.3.2.1", 77, dict(opcode=0x01, psn=1),
+                                     payload=bytes(range(256)) * ((L - 44) // 256 + 1)))
+        del fr[L:]
+        fr[2:4] = L.to_bytes(2, "big")
+        sb = np.zeros(n * stride, np.uint8)
+        rows = np.lib.stride_tricks.as_strided(sb, (n, L), (stride, 1))
+        rows[:] = np.frombuffer(bytes(fr), np.uint8)
+        rows[:, 40] = np.arange(n, dtype=np.uint8)  # distinct frames (first payload byte)
+        w, _ = oracle_batch(sb, stride=stride, length=L, n=n)
+        engine.set_lanes(lanes)
+        try:
+            g, s2 = engine.compute_strided(sb, stride, L, n)
+        finally:
+            engine.set_lanes(0)
+        np.testing.assert_array_equal(g, w, err_msg=f"L {L} stride {stride}")
