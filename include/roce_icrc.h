@@ -199,8 +199,11 @@ int ricrc_verify_strided_dev(ricrc_ctx* ctx, const uint8_t* d_frames, uint64_t s
  *
  * Output: packet p (WR order, packet order) is the wire frame at
  * frames + p * slot_bytes, lens[p] bytes long (0 with status
- * RICRC_PKT_SEG_BAD when its WR is invalid); slot bytes past the frame end, up
- * to the next 16-byte boundary, are written as zeros.
+ * RICRC_PKT_SEG_BAD when its WR is invalid).  Slot bytes past the frame end
+ * are written as zeros up to the end of the frame's last 16*G-byte run (G =
+ * lanes per packet: the next 128-byte boundary at 8 lanes; at least the next
+ * 16-byte boundary), never past the slot; later slot bytes are left as they
+ * were.
  */
 #define RICRC_SEG_SEND 0
 #define RICRC_SEG_SEND_WITH_IMM 1
@@ -243,7 +246,7 @@ typedef struct ricrc_seg_wr {
 
 /* Host-only planning (no GPU): checks every WR's op, fills wrs[i].first_pkt
  * with the running packet count, returns the total packets and the slot size
- * (the largest frame for `pmtu`, rounded up to 256 bytes).  pmtu: 256, 512,
+ * (the largest frame for `pmtu`, rounded up to 128 bytes).  pmtu: 256, 512,
  * 1024, 2048 or 4096 (IB MTU). */
 int ricrc_segment_plan(ricrc_seg_wr* wrs, uint32_t nwr, uint32_t pmtu, uint32_t* npkts_out,
                        uint32_t* slot_bytes_out);
@@ -256,7 +259,7 @@ int ricrc_segment(ricrc_ctx* ctx, const uint8_t* mr, size_t mr_bytes, const ricr
                   uint8_t* status_out /* nullable */);
 /* Device-resident, asynchronous on `stream`: d_mr (mr_bytes) and d_wrs
  * (planned on the host, then copied) are device pointers; frames go to
- * d_frames + p * slot_bytes (slot_bytes: multiple of 256, >= the plan's;
+ * d_frames + p * slot_bytes (slot_bytes: multiple of 128, >= the plan's;
  * d_frames 256-byte aligned).  d_lens doubles as the packet -> WR map while
  * the call runs.  WRs are validated on the device (status RICRC_PKT_SEG_BAD,
  * length 0).  No byte outside [d_mr, d_mr + mr_bytes) is read, except that an

@@ -321,9 +321,12 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
 }
 
 // Segmentation: the largest frame of a PMTU (IPv4 20 + UDP 8 + BTH 12 +
-// RETHImmDt 20 + payload + ICRC 4), rounded up to 256 bytes so every slot
-// starts at grid column 0 for up to 16 lanes per packet.
-uint32_t seg_slot_bytes(uint32_t pmtu) { return (60u + pmtu + 4u + 255u) & ~255u; }
+// RETHImmDt 20 + payload + ICRC 4), rounded up to whole 128-byte lines, so
+// every slot starts on a line and a frame's lines are written whole.  (Round
+// 3: 256-byte rounding, 4352 B at 4 KiB PMTU, left 212 B of every slot
+// unwritten; the write stream over 4224-byte slots runs 6 % faster,
+// scratch/seg_copy.hip: 4954 -> 5258 GB/s for the copy pattern alone.)
+uint32_t seg_slot_bytes(uint32_t pmtu) { return (60u + pmtu + 4u + 127u) & ~127u; }
 
 // Ops whose packets carry MR bytes (the rest are header-only, one packet).
 bool seg_has_payload(uint32_t op) { return op <= RICRC_SEG_READ_RESPONSE; }
@@ -335,7 +338,7 @@ bool valid_pmtu(uint32_t pmtu) {
 // Lanes per packet for segmentation (1 lane is not instantiated: the UDP
 // checksum chunk and the header need G >= 2; G <= 16 keeps the slot grid).
 int seg_log2g(const ricrc_ctx* c, uint32_t pmtu) {
-  int l = c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(seg_slot_bytes(pmtu) - 192u);
+  int l = c->lanes > 0 ? log2_lanes(c->lanes) : auto_log2g(((64u + pmtu + 255u) & ~255u) - 192u);
   return l < 1 ? 1 : l > 4 ? 4 : l;
 }
 
@@ -857,7 +860,7 @@ int ricrc_segment_dev(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes,
                       uint8_t* d_status, void* stream) {
   if (!c || !valid_pmtu(pmtu) || (nwr && !d_wrs) || (mr_bytes && !d_mr)) return RICRC_EINVAL;
   if (npkts == 0) return RICRC_OK;
-  if (!d_frames || !d_lens || (slot_bytes & 255u) || slot_bytes < seg_slot_bytes(pmtu) ||
+  if (!d_frames || !d_lens || (slot_bytes & 127u) || slot_bytes < seg_slot_bytes(pmtu) ||
       ((uintptr_t)d_frames & 255u))
     return RICRC_EINVAL;
   return seg_launch(c, d_mr, mr_bytes, d_wrs, nwr, pmtu, npkts, d_frames, slot_bytes, d_lens,

@@ -15,7 +15,7 @@
 //
 // One pass: a group of G lanes owns one packet; the packet's frame is laid on
 // the same dword grid as the ICRC kernel (icrc_kernels.hip) with the frame
-// starting at grid column 0 (slots are 256-byte aligned), so in iteration j
+// starting at grid column 0 (slots are whole 128-byte lines), so in iteration j
 // lane i produces the 16 frame bytes of dwords 4Gj + 4i .. +3: header dwords
 // from the WR descriptor, payload dwords with one (unaligned) 16-byte MR load,
 // stores them with one aligned 16-byte store and folds them into its four CRC
@@ -471,7 +471,10 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
           Y[u] = ldmr(s.src + 4 * m);
       }
       ld_block(1, X);
-      // block 0 carries the header (hd <= 15 < DPI * U)
+      // block 0 carries the header (hd <= 15 < DPI * U).  A whole buffer is
+      // refilled before the other one is used; refilling each chunk right
+      // after its use (loads in flight near 2U throughout) measured 3 %
+      // slower, also at U = 3 and 5 (3 A/B rounds, round 3).
 #pragma unroll
       for (int u = 0; u < U; ++u) edge(u, Y[u], std::true_type{});
       for (int b = 1; b < nbmax; b += 2) {
@@ -515,13 +518,12 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
         h.z = t == 2 ? icrc : h.z;
         h.w = t == 3 ? icrc : h.w;
       }
-#ifdef RICRC_SEG_WHOLE_LINES  // experiment: the last line written whole (zeros past the frame)
-      stg128<kSegStorePol>(s.dst + 16 * gl, hold0);
-      if (jl > 0) stg128<kSegStorePol>(s.dst + 4 * idxL, holdL);
-#else
-      if (4 * gl < s.T) stg128<kSegStorePol>(s.dst + 16 * gl, hold0);
-      if (jl > 0 && idxL < s.T) stg128<kSegStorePol>(s.dst + 4 * idxL, holdL);
-#endif
+      // the first and last iterations are stored whole (zeros past the frame
+      // end, never past the slot): the frame's last line goes out as one full
+      // line (+0.5 % over stopping at the 16-byte chunk holding the ICRC,
+      // 3 A/B rounds on 128-byte slots, round 3)
+      if (16 * gl < (int)a.slot) stg128<kSegStorePol>(s.dst + 16 * gl, hold0);
+      if (jl > 0 && 4 * idxL < (int)a.slot) stg128<kSegStorePol>(s.dst + 4 * idxL, holdL);
     }
     if (pkt < a.npkts && gl == 0) {
       a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;

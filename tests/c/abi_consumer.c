@@ -66,7 +66,7 @@ int main(void) {
   wrs[1].length = 0;
   uint32_t npkts = 0, slot = 0;
   if (ricrc_segment_plan(wrs, 2, 4096, &npkts, &slot) != RICRC_OK) return 3;
-  if (npkts != 4 || wrs[1].first_pkt != 3 || slot % 256 != 0) return 4;
+  if (npkts != 4 || wrs[1].first_pkt != 3 || slot % 128 != 0) return 4;
   if (ricrc_segment_plan(wrs, 2, 1000, &npkts, &slot) != RICRC_EINVAL) return 5;
   ricrc_ctx* ctx = NULL;
   int rc = ricrc_ctx_create(0, &ctx);

@@ -79,7 +79,7 @@ def test_header_is_plain_c_and_links(tmp_path):
     if torch.cuda.is_available():
         pytest.skip("GPU visible: the run leg is tests/test_gpu_capi.py")
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
-    assert out.startswith("abi 3 ok: 4 packets, slot 4352"), out
+    assert out.startswith("abi 3 ok: 4 packets, slot 4224"), out
     assert "gpu leg skipped" in out
 
 

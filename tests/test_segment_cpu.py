@@ -27,7 +27,7 @@ def test_plan_matches_compute_wr_pkt_num(pmtu):
     counts = [SO.wr_pkt_num(n, pmtu) for n in lens]
     assert npkts == sum(counts)
     assert list(rec["first_pkt"]) == list(np.concatenate([[0], np.cumsum(counts)[:-1]]))
-    assert slot % 256 == 0 and slot >= 60 + pmtu + 4 and slot - (60 + pmtu + 4) < 256
+    assert slot % 128 == 0 and slot >= 60 + pmtu + 4 and slot - (60 + pmtu + 4) < 128
 
 
 def test_plan_rejects_bad_arguments():
