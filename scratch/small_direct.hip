@@ -32,12 +32,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int MODE, int NW, int RING, int LPOL, int SPOL>
+template <int MODE, int NW, int RING, int LPOL, int SPOL, int BF = 64>
 __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t S, uint32_t n,
                                                  uint32_t* out, uint32_t* sink) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nchunk = 4 * S;
-  const uint32_t nb = (n + 63) / 64;
+  constexpr int CB = (BF * 108 + 1023) / 1024;  // loads per lane per batch (108-B frames)
+  const uint32_t nchunk = BF * S / 16;
+  const uint32_t nb = (n + BF - 1) / BF;
   const uint32_t per_block = (nb + gridDim.x - 1) / gridDim.x;
   const uint32_t b0 = blockIdx.x * per_block, b1 = min(nb, b0 + per_block);
   const uint32_t nrounds = b1 > b0 ? (b1 - b0 + NW - 1) / NW : 0;
@@ -52,9 +53,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t
       for (int t = 0; t < C; ++t)
         R[t] = __builtin_amdgcn_raw_buffer_load_b128(fr, f + 16u * t, 0, LPOL);
     } else {
-      const uint32_t base = b * 64u * S;
+      const uint32_t base = b * (uint32_t)BF * S;
 #pragma unroll
-      for (int t = 0; t < C; ++t)
+      for (int t = 0; t < CB; ++t)
         R[t] = __builtin_amdgcn_raw_buffer_load_b128(fr, base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1), 0,
                                                      LPOL);
     }
@@ -66,9 +67,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     __asm__ __volatile__("" ::: "memory");
-    const uint32_t words = min(in_ring * NW, b1 - rbase) * 64u;
+    const uint32_t words = min(in_ring * NW, b1 - rbase) * (uint32_t)BF;
     for (uint32_t i = tid; i < words / 4; i += NW * 64)
-      __builtin_amdgcn_raw_buffer_store_b128(*(const lds_u32x4*)(uintptr_t)(16u * i), orr, 4u * (rbase * 64u) + 16u * i, 0,
+      __builtin_amdgcn_raw_buffer_store_b128(*(const lds_u32x4*)(uintptr_t)(16u * i), orr, 4u * (rbase * (uint32_t)BF) + 16u * i, 0,
                                              SPOL);
     __asm__ __volatile__("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -80,14 +81,14 @@ __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t
   auto consume = [&](uint32_t r, u32x4* R) {
     u32x4 v = R[0];
 #pragma unroll
-    for (int t = 1; t < C; ++t) v ^= R[t];
+    for (int t = 1; t < (kDirect ? C : CB); ++t) v ^= R[t];
     const uint32_t w = v.x ^ v.y ^ v.z ^ v.w;
     const uint32_t b = b0 + r * NW + wave;
     load(b + 2 * NW, R);
     if constexpr (!kRing) {
       acc ^= w;
     } else {
-      *(lds_u32*)(uintptr_t)(4u * (in_ring * NW * 64u + wave * 64u + lane)) = w;
+      if (lane < BF) *(lds_u32*)(uintptr_t)(4u * (in_ring * NW * BF + wave * BF + lane)) = w;
       if (++in_ring == RING) flush();
     }
   };
@@ -142,28 +143,24 @@ int main() {
     printf("%-48s med %.4f ms  min %.4f  %.1f GB/s alg\n", name, ts[15], ts[0], rb / ts[15] / 1e6);
     fflush(stdout);
   };
-#define RUN(M, W, RG, LP, SP, NAME)                                                                 \
+#define RUN(M, W, RG, LP, SP, NAME, BF)                                                            \
   {                                                                                                 \
-    auto kf = rw<M, W, RG, LP, SP>;                                                                 \
-    const size_t lds = (size_t)(RG > 0 ? RG : 1) * W * 256;                                         \
+    auto kf = rw<M, W, RG, LP, SP, BF>;                                                             \
+    const size_t lds = (size_t)(RG > 0 ? RG : 1) * W * BF * 4;                                      \
     CK(hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
     run(NAME, [&] { hipLaunchKernelGGL(kf, dim3(ncu), dim3(64 * W), lds, 0, d, S, n, out, sink); }); \
   }
   for (int rep = 0; rep < 2; ++rep) {
-    RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt")
-    RUN(1, 12, 0, 2, 16, "direct read-only 12w nt")
-    RUN(1, 12, 0, 0, 16, "direct read-only 12w plain")
-    RUN(1, 8, 0, 2, 16, "direct read-only 8w nt")
-    RUN(1, 16, 0, 2, 16, "direct read-only 16w nt")
-    RUN(2, 12, 13, 2, 16, "coalesced + ring 13 sc1 12w")
-    RUN(3, 12, 13, 2, 16, "direct + ring 13 sc1 12w")
-    RUN(3, 12, 26, 2, 16, "direct + ring 26 sc1 12w")
-    RUN(3, 12, 40, 2, 16, "direct + ring 40 sc1 12w")
-    RUN(3, 12, 50, 2, 16, "direct + ring 50 sc1 12w")
-    RUN(3, 12, 50, 2, 2, "direct + ring 50 nt 12w")
-    RUN(3, 16, 38, 2, 16, "direct + ring 38 sc1 16w")
-    RUN(3, 8, 76, 2, 16, "direct + ring 76 sc1 8w")
-    run("write only 64 MiB", [&] { hipLaunchKernelGGL(write_only, dim3(ncu), dim3(1024), 0, 0, out, (uint64_t)n / 4); });
+    RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt", 64)
+    RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt 32-frame", 32)
+    RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt 16-frame", 16)
+    RUN(2, 12, 13, 2, 16, "coalesced + ring 13 sc1 12w", 64)
+    RUN(2, 12, 20, 2, 16, "coalesced + ring 20 sc1 12w", 64)
+    RUN(2, 12, 27, 2, 16, "coalesced + ring 27 sc1 12w", 64)
+    RUN(2, 12, 40, 2, 16, "coalesced + ring 40 sc1 12w", 64)
+    RUN(2, 12, 54, 2, 16, "coalesced + ring 54 sc1 12w 32-frame", 32)
+    RUN(2, 12, 108, 2, 16, "coalesced + ring 108 sc1 12w 16-frame", 16)
+    RUN(2, 16, 40, 2, 16, "coalesced + ring 40 sc1 16w 32-frame", 32)
   }
   return 0;
 }

@@ -1,5 +1,6 @@
 """GPU parity of the lane-per-packet kernel for small strided frames
-(stride <= 128 B, automatic lanes): batch boundaries, strides with gaps,
+(stride <= 128 B, automatic lanes; strides past 64 B run 32-frame batches with
+two lanes per frame, every front pad 0-3 below): batch boundaries, strides with gaps,
 IPv4 options (the generic-mask path), malformed frames, verify mode, and
 agreement with the lane-group kernels on the same bytes."""
 import numpy as np
@@ -35,8 +36,9 @@ def _strided(n, L, stride, rng, ihl6_every=0, bad_every=0):
     return buf
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 1023, 4099])
-@pytest.mark.parametrize("L,stride", [(48, 48), (108, 108), (108, 112), (64, 128), (128, 128)])
+@pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 63, 64, 65, 255, 257, 1023, 4099])
+@pytest.mark.parametrize("L,stride", [(48, 48), (108, 108), (108, 112), (64, 128), (128, 128),
+                                      (68, 68), (72, 72), (76, 80), (80, 84), (100, 100), (124, 128)])
 def test_small_kernel_matches_oracle(engine, n, L, stride):
     rng = np.random.default_rng(n * 1000 + L + stride)
     buf = _strided(n, L, stride, rng)
