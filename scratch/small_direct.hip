@@ -32,7 +32,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int MODE, int NW, int RING, int LPOL, int SPOL, int BF = 64>
+template <int MODE, int NW, int RING, int LPOL, int SPOL, int BF = 64, int VR = 0>
 __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t S, uint32_t n,
                                                  uint32_t* out, uint32_t* sink) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -61,13 +61,24 @@ __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t
     }
   };
   uint32_t acc = 0, in_ring = 0, rbase = b0;
+  uint32_t vr[VR > 0 ? VR : 1];  // mode 4: the last VR rounds of a window in VGPRs (vr[0] newest)
   const auto orr = rsrc(out, n * 4u);
   auto flush = [&]() {
     __asm__ __volatile__("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     __asm__ __volatile__("" ::: "memory");
-    const uint32_t words = min(in_ring * NW, b1 - rbase) * (uint32_t)BF;
+    const uint32_t lds_rounds = min(in_ring, (uint32_t)RING);
+    const uint32_t words = min(lds_rounds * NW, b1 - rbase) * (uint32_t)BF;
+    if constexpr (VR > 0) {  // rounds RING .. in_ring - 1 from the registers, 256 B per store
+#pragma unroll
+      for (int k = 0; k < VR; ++k) {
+        const uint32_t r = in_ring - 1u - (uint32_t)k;
+        const uint32_t bb = rbase + r * NW + wave;
+        if (r >= (uint32_t)RING && r < in_ring && bb < b1)
+          __builtin_amdgcn_raw_buffer_store_b32(vr[k], orr, 4u * (bb * 64u + lane), 0, SPOL);
+      }
+    }
     for (uint32_t i = tid; i < words / 4; i += NW * 64)
       __builtin_amdgcn_raw_buffer_store_b128(*(const lds_u32x4*)(uintptr_t)(16u * i), orr, 4u * (rbase * (uint32_t)BF) + 16u * i, 0,
                                              SPOL);
@@ -88,8 +99,19 @@ __global__ void __launch_bounds__(64 * NW, 1) rw(const uint8_t* frames, uint32_t
     if constexpr (!kRing) {
       acc ^= w;
     } else {
-      if (lane < BF) *(lds_u32*)(uintptr_t)(4u * (in_ring * NW * BF + wave * BF + lane)) = w;
-      if (++in_ring == RING) flush();
+      if constexpr (VR > 0) {
+        if (in_ring < (uint32_t)RING) {
+          *(lds_u32*)(uintptr_t)(4u * (in_ring * NW * BF + wave * BF + lane)) = w;
+        } else {
+#pragma unroll
+          for (int k = VR - 1; k > 0; --k) vr[k] = vr[k - 1];
+          vr[0] = w;
+        }
+        if (++in_ring == RING + VR) flush();
+      } else {
+        if (lane < BF) *(lds_u32*)(uintptr_t)(4u * (in_ring * NW * BF + wave * BF + lane)) = w;
+        if (++in_ring == RING) flush();
+      }
     }
   };
   if (nrounds) {
@@ -143,24 +165,21 @@ int main() {
     printf("%-48s med %.4f ms  min %.4f  %.1f GB/s alg\n", name, ts[15], ts[0], rb / ts[15] / 1e6);
     fflush(stdout);
   };
-#define RUN(M, W, RG, LP, SP, NAME, BF)                                                            \
+#define RUN(M, W, RG, LP, SP, NAME, BF, ...)                                                            \
   {                                                                                                 \
-    auto kf = rw<M, W, RG, LP, SP, BF>;                                                             \
+    auto kf = rw<M, W, RG, LP, SP, BF, ##__VA_ARGS__>;                                                             \
     const size_t lds = (size_t)(RG > 0 ? RG : 1) * W * BF * 4;                                      \
     CK(hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
     run(NAME, [&] { hipLaunchKernelGGL(kf, dim3(ncu), dim3(64 * W), lds, 0, d, S, n, out, sink); }); \
   }
   for (int rep = 0; rep < 2; ++rep) {
     RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt", 64)
-    RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt 32-frame", 32)
-    RUN(0, 12, 0, 2, 16, "coalesced read-only 12w nt 16-frame", 16)
     RUN(2, 12, 13, 2, 16, "coalesced + ring 13 sc1 12w", 64)
-    RUN(2, 12, 20, 2, 16, "coalesced + ring 20 sc1 12w", 64)
     RUN(2, 12, 27, 2, 16, "coalesced + ring 27 sc1 12w", 64)
-    RUN(2, 12, 40, 2, 16, "coalesced + ring 40 sc1 12w", 64)
-    RUN(2, 12, 54, 2, 16, "coalesced + ring 54 sc1 12w 32-frame", 32)
-    RUN(2, 12, 108, 2, 16, "coalesced + ring 108 sc1 12w 16-frame", 16)
-    RUN(2, 16, 40, 2, 16, "coalesced + ring 40 sc1 16w 32-frame", 32)
+    RUN(2, 12, 13, 2, 16, "coalesced + ring 13 + 8 vgpr sc1 12w", 64, 8)
+    RUN(2, 12, 13, 2, 16, "coalesced + ring 13 + 14 vgpr sc1 12w", 64, 14)
+    RUN(2, 12, 13, 2, 2, "coalesced + ring 13 + 14 vgpr nt 12w", 64, 14)
+    RUN(2, 12, 13, 2, 0, "coalesced + ring 13 + 14 vgpr plain 12w", 64, 14)
   }
   return 0;
 }

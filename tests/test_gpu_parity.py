@@ -529,6 +529,25 @@ def test_full_size_cfg5_small_bit_exact(engine):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
 
 
+@pytest.mark.parametrize("n", [256 * 486 * 64 - 1000, 256 * 458 * 64 + 77])
+def test_small_kernel_many_ring_windows(engine, n):
+    """~7.5 M 108-B frames put 40.5 / 38.2 rounds of 12 batches on each
+    workgroup of the small kernel: several full output-ring windows, then a
+    last window ending with a round that only some waves of the workgroup
+    have.  (Round 3 measured a register extension of the window here,
+    scratch/attic/small_register_rounds.diff; this case caught its first
+    version, whose idle waves skipped a shift.)"""
+    torch = pytest.importorskip("torch")
+    buf, stride, flen = synth.uniform_frames(n, 64, seed=0x5A11)
+    want, _ = oracle_batch(buf, stride=stride, length=flen, n=n)
+    d = torch.from_numpy(buf).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.compute_strided_dev(d, stride, flen, n, out, stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
 @pytest.mark.parametrize("payload,stride", [(4, 48), (76, 128)])
 def test_small_kernel_ring_regions(engine, payload, stride):
     """The small-frame kernel's output ring starts in the free halves of its
