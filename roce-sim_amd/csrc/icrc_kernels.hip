@@ -1522,6 +1522,7 @@ kernel_fn pick_small(int outs) {
 
 kernel_fn select_small(int C, bool verify, int outs) {
   if (C == 4) return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
+  if (C == 7) return verify ? pick_small<7, true>(outs) : pick_small<7, false>(outs);
   return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
 }
 
@@ -1543,7 +1544,7 @@ hipError_t prepare_kernels() {
                                            (int)lds_bytes(l, r));
         if (e != hipSuccess) return e;
       }
-  for (int c : {4, 8})
+  for (int c : {4, 7, 8})
     for (int v = 0; v < 2; ++v)
       for (int o = 0; o < 4; ++o) {
         hipError_t e = hipFuncSetAttribute((const void*)select_small(c, v, o),
@@ -1580,7 +1581,15 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
 hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   if (a.stride > kSmallMaxStride || (a.stride & 3u) || a.stride == 0) return hipErrorInvalidValue;
-  const int C = a.stride <= 64 ? 4 : 8;  // 16-byte loads per lane per batch (4 * stride / 64)
+  // 16-byte loads per lane per batch (>= 4 * stride / 64).  C = 7 up to 112-B
+  // strides (cfg5, 108 B: 432 chunks): with C = 8 every lane's 8th load and
+  // LDS write were copies of the batch's last chunk (64 lanes writing one
+  // 16-byte LDS address)
+#ifndef RICRC_SMALL_NO_C7
+  const int C = a.stride <= 64 ? 4 : a.stride <= 112 ? 7 : 8;
+#else
+  const int C = a.stride <= 64 ? 4 : 8;
+#endif
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
   kernel_fn k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;
