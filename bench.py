@@ -140,6 +140,39 @@ def cpu_share() -> tuple[int, dict]:
                            "host_cpus": os.cpu_count()}
 
 
+def cpu_native_c(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: np.ndarray,
+                 threads: int) -> dict:
+    """The oracle's C restatement (oracle/icrc_ref.c: masked copy + slice-by-8
+    CRC-32 per frame, pthreads) over the same host frames: what a native CPU
+    port of BTH.compute_icrc reaches on this job's cores, beside the Python
+    per-packet path the reference runs.  Whole batch, repeated to ~0.5 s."""
+    import ctypes
+    path = ROOT / "oracle" / "build" / "liboracle.so"
+    if not path.exists():
+        return {"native_c_note": f"{path.name} not built (make -C oracle)"}
+    lib = ctypes.CDLL(str(path))
+    lib.oracle_icrc_batch.restype = ctypes.c_int
+    lib.oracle_icrc_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    n = offs.size
+    out = np.zeros(n, np.uint32)
+    passes, t = 0, 0.0
+    while passes == 0 or (t < 0.5 and passes < 8):
+        t0 = time.perf_counter()
+        rc = lib.oracle_icrc_batch(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, 0, 0, n,
+                                   out.ctypes.data, None, threads)
+        t += time.perf_counter() - t0
+        passes += 1
+        if rc != 0:
+            return {"native_c_note": f"oracle_icrc_batch failed ({rc})"}
+    cov = int((lens.astype(np.int64) - 4).sum())
+    return {"native_c_GiBps": round(passes * cov / t / 2**30, 3), "native_c_threads": threads,
+            "native_c_mismatches_vs_gpu": int((out != gpu_icrc).sum())}
+
+
 def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: np.ndarray):
     """Per-packet zlib restatement (oracle/, the CPU "port" baseline) on this host.
 
@@ -172,6 +205,8 @@ def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: 
             passes += 1
     allc = np.concatenate(parts)
     mism = int((allc != gpu_icrc).sum()) + int((one != gpu_icrc[:n1]).sum())
+    native = cpu_native_c(buf, offs, lens, gpu_icrc, procs)
+    mism += native.get("native_c_mismatches_vs_gpu", 0)
     c_all, c_one = int(cov.sum()), int(cov[:n1].sum())
     return {
         "value": round(passes * c_all / tn / 2**30, 4),
@@ -190,6 +225,7 @@ def cpu_baseline(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_icrc: 
         "single_core_x_affinity_GiBps": round(c_one / t1 / 2**30 * share["affinity_cpus"], 2),
         "cpu_model": cpu_model(),
         "parity_mismatches_vs_gpu": mism,
+        **native,
     }
 
 

@@ -45,9 +45,11 @@ else
   # FETCH_SIZE factor measured on this workload's own access pattern (scripts/fetch_calib.py)
   CAL=""
   CF=$R/profiles/r03b_fetch_calibration/$WL.json
+  # cfg4's shard runs cfg2's kernel on cfg2-shaped frames: the same pattern
+  [ "$WL" = cfg4 ] && CF=$R/profiles/r03b_fetch_calibration/cfg2.json
   if [ -f $CF ]; then
     F=$(python3 -c "import json; print(json.load(open('$CF'))['factor'])")
-    CAL="--calibration $F --calibration-source profiles/r03b_fetch_calibration/$WL.json"
+    CAL="--calibration $F --calibration-source ${CF#$R/}"
   fi
   python3 scripts/pmc_traffic.py --fetch $OUT/pmcf_$TAG --write $OUT/pmcw_$TAG --workload $WL \
     --packets $NP --frame-bytes 0 --ceiling-read-bytes $BUF --alg-bytes $ALG --kernel "$KN" $CAL \

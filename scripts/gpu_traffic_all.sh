@@ -4,7 +4,7 @@
 set -u
 TAG=${1:-r03}
 shift || true
-WLS=${*:-cfg2 cfg3 cfg5 seg}
+WLS=${*:-cfg2 cfg3 cfg5 seg cfg4}
 for WL in $WLS; do
   echo "==== $WL"
   SKIP_TESTS=1 bash scripts/gpu_profile.sh ${TAG}_$WL $WL || exit $?
