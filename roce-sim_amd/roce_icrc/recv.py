@@ -36,6 +36,7 @@ import logging
 import socket
 import struct
 import time
+from collections import deque
 from dataclasses import dataclass, field
 from typing import Callable, Iterable, Optional
 
@@ -237,12 +238,12 @@ class RecvLoop:
         self.verify = verify or verify_frames
         self.keep_dropped = keep_dropped
         self.stats = RecvStats()
-        self._pending: list[BTH] = []  # verified packets not yet handed out
+        self._pending: deque[BTH] = deque()  # verified packets not yet handed out
 
-    def _fill(self) -> None:
+    def _fill(self, timeout: Optional[float] = -1.0) -> None:
         # up to `batch` datagrams per verify launch (the ones a source already
         # holds; a raw socket waits only for the first)
-        dg = self.source.recv_batch(self.batch, self.timeout)
+        dg = self.source.recv_batch(self.batch, self.timeout if timeout == -1.0 else timeout)
         self.stats.datagrams += len(dg)
         roce = [d for d in dg if roce_udp_dport(d) == ROCE_PORT]
         self.stats.not_roce += len(dg) - len(roce)
@@ -268,17 +269,28 @@ class RecvLoop:
         expects the timeout and returns [].  A source running dry raises
         ``socket.timeout`` as ``recvfrom`` does."""
         if npkt == 0:
-            try:
-                self._fill()
-            except socket.timeout:
-                return []
-            raise AssertionError("BUG: just wait for timeout and it should not receive any packet")
+            # the reference's socket is bound to the RoCE port and does not
+            # verify: what it would receive is a RoCE datagram that passes the
+            # ICRC; other datagrams a raw source sees, and frames dropped for
+            # their ICRC, do not end the wait
+            deadline = None if self.timeout is None else time.monotonic() + self.timeout
+            while True:
+                left = None if deadline is None else deadline - time.monotonic()
+                if left is not None and left <= 0:
+                    return []
+                try:
+                    self._fill(left)
+                except socket.timeout:
+                    return []
+                if self._pending:
+                    raise AssertionError(
+                        "BUG: just wait for timeout and it should not receive any packet")
         out = []
         while len(out) < npkt:
             if not self._pending:
                 self._fill()
                 continue
-            pkt = self._pending.pop(0)
+            pkt = self._pending.popleft()
             if qpn is not None and pkt.dqpn != qpn:
                 self.stats.other_qp += 1
                 logging.warning("expected qpn: %s, received pkt's qpn: %s", qpn, pkt.dqpn)

@@ -57,6 +57,15 @@ def test_npkt_zero_expects_the_timeout():
     assert RV.RecvLoop(RV.ListSource([]), verify=oracle_verify).recv_pkts(0) == []
     with pytest.raises(AssertionError):
         RV.RecvLoop(RV.ListSource(_frames(1)), verify=oracle_verify).recv_pkts(0)
+    # what the reference's port-4791 socket would not see (other UDP ports)
+    # and frames dropped for their ICRC do not end the wait for the timeout
+    bad = _frames(2)[1]
+    bad = bad[:60] + bytes([bad[60] ^ 4]) + bad[60:][1:]
+    stray = o.build_frame("127.0.0.1", "127.0.0.1", 9, dict(opcode=0x01, psn=0, dqpn=0x21),
+                          payload=bytes(8), dport=5000)
+    loop = RV.RecvLoop(RV.ListSource([stray, bad, stray]), batch=1, verify=oracle_verify)
+    assert loop.recv_pkts(0) == []
+    assert loop.stats.not_roce == 2 and loop.stats.icrc_dropped == 1
 
 
 def _raw_pair():
