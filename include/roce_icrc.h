@@ -107,11 +107,17 @@ void* ricrc_ctx_stream(ricrc_ctx* ctx);
 int ricrc_compute_one(ricrc_ctx* ctx, const uint8_t* frame, size_t len, uint32_t* icrc_out,
                       uint8_t* status_out /* nullable */);
 /* Idle timeout of the per-packet service in microseconds (default 1000);
- * 0 turns the service off (ricrc_compute_one then launches a kernel per call). */
+ * 0 turns the service off (ricrc_compute_one and small bursts then launch a
+ * kernel per call). */
 int ricrc_ctx_set_service(ricrc_ctx* ctx, uint32_t idle_us);
 
 /* Ragged batch: frame i is frames[offsets[i] .. offsets[i] + lens[i]).
- * `frames_bytes` is the size of the `frames` buffer (bounds for the copy). */
+ * `frames_bytes` is the size of the `frames` buffer (bounds for the copy).
+ * A small burst (up to 64 frames, 64 KiB packed; automatic lanes) goes to the
+ * same resident wave as ricrc_compute_one, as one request (the wave copies
+ * the packed frames into LDS and folds eight at a time); larger batches, a
+ * context whose service is off, or an explicit lanes setting launch the
+ * kernels (copy in, kernel, copy out). */
 int ricrc_compute_batch(ricrc_ctx* ctx, const uint8_t* frames, size_t frames_bytes,
                         const uint64_t* offsets, const uint32_t* lens, uint32_t n,
                         uint32_t* icrc_out, uint8_t* status_out /* nullable */);

@@ -284,6 +284,14 @@ int host_ragged_staged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,
   return RICRC_OK;
 }
 
+int service_burst(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offsets,
+                  const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,
+                  uint8_t* ok_out, bool verify);
+#ifndef RICRC_SVC_BURST_ROUTE
+#define RICRC_SVC_BURST_ROUTE 64
+#endif
+constexpr uint32_t kSvcBurstRoute = RICRC_SVC_BURST_ROUTE;  // host batches up to this many frames
+
 int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const uint64_t* offsets,
                 const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,
                 uint8_t* ok_out, bool verify) {
@@ -294,6 +302,16 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
   for (uint32_t i = 0; i < n; ++i)
     if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
+  // a burst of up to 64 frames (64 KiB packed) goes to the resident wave
+  // (automatic lanes only: an explicit lanes setting asks for the kernels)
+  if (c->svc_idle_us && c->lanes == 0 && n <= kSvcBurstRoute) {
+    uint64_t packed = 0;
+    for (uint32_t i = 0; i < n; ++i) packed += ((uint64_t)lens[i] + 3u) & ~(uint64_t)3u;
+    if (packed <= ricrc::kSvcMaxFrame) {
+      const int rc = service_burst(c, frames, offsets, lens, n, icrc_out, status_out, ok_out, verify);
+      if (rc != RICRC_EIO) return rc;  // (no answer within 1 s: the launch path below)
+    }
+  }
   if (frames_bytes <= kStageMaxFrames && 32ull * n + 1536 <= kStageBytes - up256(frames_bytes))
     return host_ragged_staged(c, frames, frames_bytes, offsets, lens, n, icrc_out, status_out,
                               ok_out, verify);
@@ -465,22 +483,22 @@ int service_ensure(ricrc_ctx* c) {
   return RICRC_OK;
 }
 
-// One frame through the resident wave.  Returns RICRC_EIO (with the service
-// stopped) if no answer came within a second -- the caller then takes the
-// launch path.
-int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icrc_out,
-                 uint8_t* status_out) {
-  int rc = service_init(c);
-  if (rc) return rc;
-  rc = service_ensure(c);
-  if (rc) return rc;
+// Publishes a request whose frame bytes (and descriptors) are in the slot and
+// waits for its answer word.  Returns RICRC_EIO (with the service stopped) if
+// no answer came within a second -- the caller then takes the launch path.
+// `answer`: the single-frame answer word (resp); a burst instead waits for
+// `burst_last` (its last answer) to carry the request's tag.
+int service_request(ricrc_ctx* c, uint32_t hi, uint64_t* answer, const uint64_t* burst_last = nullptr) {
   ricrc::ServiceRing* r = c->svc;
-  std::memcpy((uint8_t*)r + ricrc::kSvcFrame, frame, len);
   const uint32_t seq = ++c->svc_seq == 0 ? ++c->svc_seq : c->svc_seq;  // (0 = nothing yet)
-  __atomic_store_n(&r->req, ((uint64_t)len << 32) | seq, __ATOMIC_RELEASE);
+  __atomic_store_n(&r->req, ((uint64_t)hi << 32) | seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   uint64_t ans = 0;
   auto answered = [&] {
+    if (burst_last) {
+      ans = __atomic_load_n(burst_last, __ATOMIC_ACQUIRE);
+      return (uint32_t)(ans >> 48) == ricrc::svc_burst_tag(seq);
+    }
     ans = __atomic_load_n(&r->resp, __ATOMIC_ACQUIRE);
     return (uint32_t)(ans >> 40) == (seq & ricrc::kSvcSeqMask);
   };
@@ -492,7 +510,7 @@ int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icr
       // launch it again (it serves the pending request first)
       if (hipStreamQuery(c->svc_stream) == hipSuccess && !answered()) {
         c->svc_launched = false;
-        rc = service_ensure(c);
+        const int rc = service_ensure(c);
         if (rc) return rc;
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
@@ -502,8 +520,83 @@ int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icr
     }
     __builtin_ia32_pause();
   }
+  if (answer) *answer = ans;
+  return RICRC_OK;
+}
+
+// One frame through the resident wave.
+int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icrc_out,
+                 uint8_t* status_out) {
+  int rc = service_init(c);
+  if (rc) return rc;
+  rc = service_ensure(c);
+  if (rc) return rc;
+  std::memcpy((uint8_t*)c->svc + ricrc::kSvcFrame, frame, len);
+  uint64_t ans = 0;
+  rc = service_request(c, len, &ans);
+  if (rc) return rc;
   *icrc_out = (uint32_t)ans;
   if (status_out) *status_out = (uint8_t)(ans >> 32);
+  return RICRC_OK;
+}
+
+// A burst of up to kSvcMaxBurst frames (packed dword-aligned, at most
+// kSvcMaxFrame bytes) through the resident wave: one request, one answer
+// word per frame (icrc_internal.hpp, ServiceRing).
+int service_burst(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offsets,
+                  const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,
+                  uint8_t* ok_out, bool verify) {
+  int rc = service_init(c);
+  if (rc) return rc;
+  rc = service_ensure(c);
+  if (rc) return rc;
+  if (n == 1) {  // one frame: the single-frame request (G = 64, no descriptor read)
+    const uint32_t L = lens[0];
+    uint32_t icrc = 0;
+    uint8_t st = 0;
+    rc = service_call(c, frames + offsets[0], L, &icrc, &st);
+    if (rc) return rc;
+    if (verify) {  // the kernels' verdict: the trailer (bytes L-4 .. L-1, little-endian)
+      uint32_t t = 0;
+      if (L >= 4) std::memcpy(&t, frames + offsets[0] + L - 4, 4);
+      const bool good = (st & RICRC_PKT_FATAL) == 0;
+      const bool ok = good && t == icrc;
+      if (good && !ok) st |= RICRC_PKT_ICRC_MISMATCH;
+      ok_out[0] = ok ? 1 : 0;
+    }
+    if (icrc_out) icrc_out[0] = icrc;
+    if (status_out) status_out[0] = st;
+    return RICRC_OK;
+  }
+  uint8_t* base = (uint8_t*)c->svc;
+  uint64_t* desc = (uint64_t*)(base + ricrc::kSvcDesc);
+  uint32_t pos = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    std::memcpy(base + ricrc::kSvcFrame + pos, frames + offsets[i], lens[i]);
+    desc[i] = pos | ((uint64_t)lens[i] << 32);
+    pos += (lens[i] + 3u) & ~3u;
+  }
+  uint64_t* res = (uint64_t*)(base + ricrc::kSvcAns);
+  std::memset(res, 0, 8ull * n);
+  // the last answer's tag ends the wait (the wave stores all of them with one
+  // instruction); every other answer is then checked for its tag as well
+  const uint32_t kib = (pos + 1023u) / 1024u;  // what the wave copies into LDS
+  rc = service_request(c, ricrc::kSvcBurst | (verify ? ricrc::kSvcVerify : 0u) | (kib << 16) | n,
+                       nullptr, res + (n - 1));
+  if (rc) return rc;
+  const uint32_t tag = ricrc::svc_burst_tag(c->svc_seq);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t v;
+    for (uint32_t spin = 0;; ++spin) {  // (normally at once)
+      v = __atomic_load_n(res + i, __ATOMIC_ACQUIRE);
+      if ((uint32_t)(v >> 48) == tag) break;
+      if (spin > (1u << 26)) return RICRC_EIO;
+      __builtin_ia32_pause();
+    }
+    if (icrc_out) icrc_out[i] = (uint32_t)v;
+    if (status_out) status_out[i] = (uint8_t)(v >> 32);
+    if (verify) ok_out[i] = (uint8_t)(v >> 40);
+  }
   return RICRC_OK;
 }
 

@@ -116,7 +116,19 @@ struct ServiceRing {
 constexpr uint32_t kSvcSeqMask = 0xFFFFFFu;
 constexpr uint32_t kSvcFrame = 1024;  // frame offset in the slot (aligned grid: 1 KiB at G = 64)
 constexpr uint32_t kSvcMaxFrame = 65536;
-constexpr size_t kSvcBytes = kSvcFrame + kSvcMaxFrame;
+// Burst requests (round 3): up to kSvcMaxBurst frames packed dword-aligned in
+// the frame region, one descriptor each (offset from kSvcFrame | length << 32)
+// and one 8-byte answer each (ICRC bits 0-31, status 32-39, verify verdict
+// 40-47, the request's tag 48-63, never 0: the host zeroes the answers before
+// it publishes, so an answer is complete when its tag matches, and no fence
+// orders answers against a flag); the request's high word is kSvcBurst |
+// (verify ? kSvcVerify : 0) | packed KiB << 16 | count.
+constexpr uint32_t kSvcMaxBurst = 64;
+__host__ __device__ inline uint32_t svc_burst_tag(uint32_t seq) { return (seq & 0x7FFFu) | 0x8000u; }
+constexpr uint32_t kSvcBurst = 0x80000000u, kSvcVerify = 0x40000000u;
+constexpr uint32_t kSvcDesc = kSvcFrame + kSvcMaxFrame;
+constexpr uint32_t kSvcAns = kSvcDesc + 8 * kSvcMaxBurst;
+constexpr size_t kSvcBytes = kSvcAns + 8 * kSvcMaxBurst;
 static_assert(sizeof(ServiceRing) == 256, "two 128-byte lines");
 
 struct ServiceArgs {

@@ -1413,20 +1413,69 @@ __global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4
 // every path through the loop reaches one of the two, so the grid always
 // drains; the host relaunches it on the next call.
 constexpr int kSvcThreads = 256;  // all stage the tables; wave 0 then serves
+// LDS of the service (round 3): Mul(8192) for single frames (G = 64) and
+// Mul(1024) for bursts (G = 8) as the two halves of the Keys8 rows (64 KiB),
+// the combine sets Mul(-32), Mul(-128 2^l), l < 6 (both widths use the
+// first ones), the fix-up LUT; then the results of a burst (ICRC words,
+// verdicts, status bytes, written through generic pointers) and a 64 KiB
+// staging area a burst's frames are copied into with LDS-DMA before they are
+// folded from LDS.
+using SvcKeysL = Keys8T<0>;  // Mul(8192), G = 64
+using SvcKeysS = Keys8T<1>;  // Mul(1024), G = 8
+constexpr uint32_t kSvcLut = kFixLut<6, SvcKeysL>;
+constexpr uint32_t kSvcOut = kSvcLut + 256u - 16u;  // single frame: ICRC + status (the LUT's spare bytes)
+constexpr uint32_t kBurstIcrc = kSvcLut + 256u;
+constexpr uint32_t kBurstOk = kBurstIcrc + 4u * kSvcMaxBurst;
+constexpr uint32_t kBurstSt = kBurstOk + kSvcMaxBurst;
+constexpr uint32_t kBurstStage = (kBurstSt + kSvcMaxBurst + 1023u) & ~1023u;
+constexpr size_t kSvcLds = kBurstStage + kSvcMaxFrame + 1024u;  // (+ the last chunk's reach)
+static_assert(kSvcLds <= 163840, "service LDS");
+
+// One burst: frame i at stage + (desc[i] & 0xFFFFFFFF), length desc[i] >> 32,
+// eight frames at a time (G = 8 groups of the wave), folded from LDS.
+template <bool VERIFY>
+__device__ __forceinline__ void serve_burst(const uint64_t* desc, uint32_t cnt, int lane) {
+  constexpr int LOG2G = 3, G = 8, DPI = 4 * G;
+  const uint64_t dl = (uint32_t)lane < cnt ? desc[lane] : 0ull;  // every descriptor in one read
+  const uint32_t dlo = (uint32_t)dl, dhi = (uint32_t)(dl >> 32);
+  const uint8_t* stage = (const uint8_t*)(__attribute__((address_space(3))) uint8_t*)(uintptr_t)kBurstStage;
+  IcrcArgs a{};
+  a.frames = stage;
+  a.n = cnt;
+  a.icrc_out = (uint32_t*)(lds_u32*)(uintptr_t)kBurstIcrc;  // flat stores into LDS
+  a.ok_out = (uint8_t*)(lds_u32*)(uintptr_t)kBurstOk;
+  a.status_out = (uint8_t*)(lds_u32*)(uintptr_t)kBurstSt;
+  const int gl = lane & (G - 1), grp = lane >> LOG2G;
+  const SvcKeysS kk = SvcKeysS::make(lane);
+  for (uint32_t s0 = 0; s0 < cnt; s0 += 64 / G) {
+    const uint32_t i = s0 + (uint32_t)grp;
+    const bool live = i < cnt;
+    const uint32_t ii = live ? i : 0u;
+    // this group's descriptor (lane ii of the wave holds it)
+    const uint32_t off = (uint32_t)__shfl((int)dlo, (int)ii, 64);
+    uint32_t L = (uint32_t)__shfl((int)dhi, (int)ii, 64);
+    if (off > kSvcMaxFrame || L > kSvcMaxFrame - off) L = 0;  // (a bad descriptor: BAD_LEN)
+    const Pkt p = describe<DPI>(stage, i, live, off, live ? L : 0u);
+    Batch<kUnroll> b = issue_packet<LOG2G, VERIFY>(p, gl);
+    finish_packet<LOG2G, VERIFY, SvcKeysS, kSvcLut>(a, p, b, gl, grp * G, kk);
+  }
+}
+
 __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArgs s) {
   constexpr int LOG2G = 6;
   constexpr int DPI = 4 << LOG2G;
   const int tid = threadIdx.x;
-  stage_tables<LOG2G, kSvcThreads, MainKeys>(s.tables, tid);
+  stage_tables<LOG2G, kSvcThreads, SvcKeysL>(s.tables, tid);
+  SvcKeysS::template stage<kSvcThreads>(s.tables + 3 * 1024, tid);  // main set 3: Mul(1024)
   __syncthreads();
   if (tid >= 64) return;
   const int lane = tid;
-  const MainKeys kk = MainKeys::make(lane);
+  const SvcKeysL kk = SvcKeysL::make(lane);
   ServiceRing* r = s.ring;
   const uint8_t* frame = (const uint8_t*)r + kSvcFrame;
   // the group's result goes to two LDS words past the tables (flat stores
   // through generic pointers), then out as one 8-byte answer
-  constexpr uint32_t kOut = (uint32_t)kFixLut<6, MainKeys> + 256u - 16u;  // (the LUT's spare bytes)
+  constexpr uint32_t kOut = kSvcOut;
   IcrcArgs a{};
   a.frames = frame;
   a.n = 1;
@@ -1442,9 +1491,52 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
       const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before req
       const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(req >> 32));
+      if (L & kSvcBurst) {
+        const uint32_t cnt = min(L & 0xFFu, kSvcMaxBurst);
+        const uint32_t kib = min((L >> 16) & 0x7Fu, kSvcMaxFrame / 1024u);  // packed KiB
+        const uint64_t* desc = (const uint64_t*)((const uint8_t*)r + kSvcDesc);
+        // the packed frames into LDS: one LDS-DMA wave-instruction per KiB, all
+        // in flight at once (one PCIe round trip)
+        for (uint32_t k = 0; k < kib; ++k)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(frame + 1024u * k + 16u * (uint32_t)lane),
+              (__attribute__((address_space(3))) void*)(uintptr_t)(kBurstStage + 1024u * k), 16, 0, 0);
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the frames are in LDS
+        __asm__ __volatile__("" ::: "memory");
+        if (cnt > 0) {
+          if (L & kSvcVerify)
+            serve_burst<true>(desc, cnt, lane);
+          else
+            serve_burst<false>(desc, cnt, lane);
+        }
+        // the results (flat and LDS stores) have landed before the lanes read them
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0);
+        __asm__ __volatile__("" ::: "memory");
+        if (lane == 0) {  // (diagnostics, before the answers: the host reads them after)
+          r->t_seen = t_seen;
+          r->t_done = __builtin_amdgcn_s_memrealtime();
+          r->polls = polls;
+        }
+        // each answer carries the request's tag: one 8-byte store per frame,
+        // no fence (the host cleared the answers before the request)
+        if ((uint32_t)lane < cnt) {
+          const uint64_t ans = (uint64_t)lds_rd(kBurstIcrc + 4u * (uint32_t)lane) |
+                               ((uint64_t)lds_rd8(kBurstSt + (uint32_t)lane) << 32) |
+                               ((uint64_t)lds_rd8(kBurstOk + (uint32_t)lane) << 40) |
+                               ((uint64_t)svc_burst_tag(seq) << 48);
+          __hip_atomic_store((uint64_t*)((uint8_t*)r + kSvcAns) + lane, ans, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        polls = 0;
+        served = seq;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        continue;
+      }
       const Pkt p = describe<DPI>(frame, 0, true, 0, L <= kSvcMaxFrame ? L : 0u);
       Batch<kUnroll> b = issue_packet<LOG2G, false>(p, lane);
-      finish_packet<LOG2G, false>(a, p, b, lane, 0, kk);
+      finish_packet<LOG2G, false, SvcKeysL, kSvcLut>(a, p, b, lane, 0, kk);
       // the flat stores of the result (through generic pointers into LDS)
       // have landed before lane 0 reads the words back with LDS reads
       __asm__ __volatile__("" ::: "memory");
@@ -1472,7 +1564,6 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane == 0) __hip_atomic_store(&r->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-constexpr size_t kSvcLds = kFixLut<6, MainKeys> + 256u;  // tables + combine sets + fix-up LUT
 
 typedef void (*kernel_fn)(IcrcArgs);
 

@@ -67,17 +67,45 @@ def main():
             eng.compute_one(frame)
             print(json.dumps({"call": "compute_one after idle exit", "frame_bytes": flen,
                               "us": round((time.perf_counter() - t0) * 1e6, 1)}), flush=True)
-    for n in (16, 256, 4096):
-        buf, offs, lens = synth.mixed_mtu_frames(n, seed=3)
-        med, p99 = med_us(lambda: eng.compute_batch(buf, offs, lens), max(20, a.reps // 4))
-        cov = synth.covered_bytes(lens)
-        print(json.dumps({"call": "compute_batch", "n": n, "median_us": round(med, 2),
-                          "p99_us": round(p99, 2), "GiBps": round(cov / med / 1e-6 / 2**30, 3)}),
-              flush=True)
-        med, p99 = med_us(lambda: eng.verify_batch(buf, offs, lens), max(20, a.reps // 4))
-        print(json.dumps({"call": "verify_batch", "n": n, "median_us": round(med, 2),
-                          "p99_us": round(p99, 2)}), flush=True)
-
+    # bursts: up to 64 frames / 64 KiB go to the resident wave as ONE request
+    # (round 3), larger batches and service 0 launch the kernels
+    acks = [orc.build_frame("10.0.0.2", "10.0.0.1", 9, dict(opcode=0x11, psn=i, dqpn=5),
+                            ext=orc.aeth_bytes(0, 31, i)) for i in range(64)]
+    abuf = np.frombuffer(b"".join(acks), np.uint8).copy()
+    aoffs = np.arange(64, dtype=np.uint64) * len(acks[0])
+    alens = np.full(64, len(acks[0]), np.uint32)
+    for service in (1000, 0):
+        eng.set_service(service)
+        cases = [("mixed-MTU", n) + synth.mixed_mtu_frames(n, seed=3) for n in (1, 4, 16, 256, 4096)]
+        cases.append(("ACK", 64, abuf, aoffs, alens))
+        for kind, n, buf, offs, lens in cases:
+            want = np.array([orc.icrc_of_frame_at(buf, int(a_), int(b_)) for a_, b_ in zip(offs, lens)],
+                            np.uint32)
+            got = []
+            med, p99 = med_us(lambda: got.append(eng.compute_batch(buf, offs, lens)[0]),
+                              max(20, a.reps // 4))
+            assert all((g == want).all() for g in got)
+            zmed, _ = med_us(lambda: [orc.icrc_of_frame_at(buf, int(a_), int(b_))
+                                      for a_, b_ in zip(offs, lens)], max(20, a.reps // 4))
+            cov = synth.covered_bytes(lens)
+            gpu = None
+            if service and n <= 64:  # GPU side of a burst request (stamps land after the answers)
+                g = []
+                for _ in range(30):
+                    eng.compute_batch(buf, offs, lens)
+                    time.sleep(0.0005)
+                    g.append(eng.service_times()[0])
+                gpu = round(float(np.median(g)), 2)
+            print(json.dumps({"call": "compute_batch", "frames": kind, "n": n, "gpu_side_median_us": gpu,
+                              "service_idle_us": service, "bytes": int(lens.sum()),
+                              "median_us": round(med, 2), "p99_us": round(p99, 2),
+                              "GiBps": round(cov / med / 1e-6 / 2**30, 3),
+                              "cpu_restatement_median_us": round(zmed, 2)}), flush=True)
+            med, p99 = med_us(lambda: eng.verify_batch(buf, offs, lens), max(20, a.reps // 4))
+            print(json.dumps({"call": "verify_batch", "frames": kind, "n": n,
+                              "service_idle_us": service, "median_us": round(med, 2),
+                              "p99_us": round(p99, 2)}), flush=True)
+    eng.set_service(1000)
 
 if __name__ == "__main__":
     main()

@@ -119,6 +119,123 @@ def test_batch_work_of_another_context_completes_beside_the_service(engine):
         engine.set_service(1000)
 
 
+def _t_done(engine):
+    """Raw real-time stamp of the last request the service answered (moves
+    with every request the wave serves)."""
+    t = np.zeros(3, np.uint64)
+    assert engine.lib.ricrc_ctx_service_times(engine.ctx, t.ctypes.data) == 0
+    return int(t[1])
+
+
+def _served_since(engine, t0, wait=0.1):
+    """A burst's diagnostics are not ordered against its answers (no fence on
+    the GPU side): give the stamp a moment to land."""
+    end = time.perf_counter() + wait
+    while _t_done(engine) == t0 and time.perf_counter() < end:
+        time.sleep(0.001)
+    return _t_done(engine) != t0
+
+
+def _burst_sets():
+    """Bursts the wave serves: the frame shapes above that fit 64 KiB
+    (malformed, odd lengths, IPv4 options, 44 B .. 9 KiB), 64 random-length
+    frames, one frame, and ACK-sized frames."""
+    fr = [f for f in _frames() if len(f) < 20000]
+    rng = np.random.default_rng(9)
+    rnd = [o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x07, psn=i, dqpn=3),
+                         payload=rng.integers(0, 256, int(rng.integers(0, 960)), dtype=np.uint8).tobytes())
+           for i in range(64)]
+    acks = [o.build_frame("10.0.0.2", "10.0.0.1", 9, dict(opcode=0x11, psn=i, dqpn=5),
+                          ext=o.aeth_bytes(0, 31, i)) for i in range(40)]
+    return [fr, rnd, rnd[:1], acks, fr + acks[:10]]
+
+
+def _pack(frames, gap=0):
+    offs, pos = [], 0
+    for f in frames:
+        offs.append(pos)
+        pos += len(f) + gap
+    buf = np.zeros(pos, np.uint8)
+    for off, f in zip(offs, frames):
+        buf[off:off + len(f)] = np.frombuffer(f, np.uint8)
+    return buf, np.array(offs, np.uint64), np.array([len(f) for f in frames], np.uint32)
+
+
+def test_burst_through_the_service_bit_exact(engine):
+    """compute_batch / verify_batch of up to 64 frames (64 KiB) are one request
+    to the resident wave (round 3): answers equal the oracle's and the launch
+    path's, statuses included; frames at any byte offset of the caller's
+    buffer (the host packs them dword-aligned)."""
+    for k, fr in enumerate(_burst_sets()):
+        buf, offs, lens = _pack(fr, gap=k % 3)
+        want = np.array([_want(f) for f in fr], np.uint32)
+        engine.set_service(1000)
+        t0 = _t_done(engine)
+        got, st = engine.compute_batch(buf, offs, lens)
+        assert _served_since(engine, t0), "the burst did not go through the service"
+        np.testing.assert_array_equal(got, want, err_msg=f"set {k}")
+        engine.set_service(0)
+        try:
+            got2, st2 = engine.compute_batch(buf, offs, lens)
+        finally:
+            engine.set_service(1000)
+        np.testing.assert_array_equal(got2, want)
+        np.testing.assert_array_equal(st, st2, err_msg=f"set {k}")
+
+
+def test_burst_verify_through_the_service(engine):
+    rng = np.random.default_rng(11)
+    fr = [bytearray(f) for f in _burst_sets()[1]]
+    for f in fr:  # correct trailers
+        f[-4:] = int(o.icrc_of_frame(bytes(f))).to_bytes(4, "little")
+    bad = rng.choice(len(fr), 9, replace=False)
+    for i in bad[:5]:
+        fr[i][len(fr[i]) - 5] ^= 0x20  # a covered, unmasked bit: must fail
+    for i in bad[5:]:
+        fr[i][1] ^= 0xFF  # TOS, a masked field: must pass
+    buf, offs, lens = _pack([bytes(f) for f in fr], gap=1)
+    engine.set_service(1000)
+    t0 = _t_done(engine)
+    ok, icrc, st = engine.verify_batch(buf, offs, lens)
+    assert _served_since(engine, t0)
+    want_ok = np.ones(len(fr), bool)
+    want_ok[bad[:5]] = False
+    np.testing.assert_array_equal(ok, want_ok)
+    np.testing.assert_array_equal(icrc, np.array([o.icrc_of_frame(bytes(f)) for f in fr], np.uint32))
+    engine.set_service(0)
+    try:
+        ok2, icrc2, st2 = engine.verify_batch(buf, offs, lens)
+    finally:
+        engine.set_service(1000)
+    np.testing.assert_array_equal(ok, ok2)
+    np.testing.assert_array_equal(st, st2)
+
+
+def test_bursts_past_the_slot_take_the_launch_path(engine):
+    """65 frames, or more than 64 KiB, or an explicit lanes setting: the
+    kernels (same answers); single frames and bursts interleave."""
+    engine.set_service(1000)
+    rng = np.random.default_rng(13)
+    fr = [o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x01, psn=i, dqpn=3),
+                        payload=rng.integers(0, 256, 900, dtype=np.uint8).tobytes()) for i in range(80)]
+    big = [o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x01, psn=i, dqpn=3),
+                         payload=rng.integers(0, 256, 9000, dtype=np.uint8).tobytes()) for i in range(8)]
+    for frames in (fr[:65], big, fr[:64]):
+        buf, offs, lens = _pack(frames)
+        got, _ = engine.compute_batch(buf, offs, lens)
+        np.testing.assert_array_equal(got, np.array([o.icrc_of_frame(f) for f in frames], np.uint32))
+        assert engine.compute_one(frames[3])[0] == o.icrc_of_frame(frames[3])
+    engine.set_lanes(8)
+    try:
+        buf, offs, lens = _pack(fr[:10])
+        t0 = _t_done(engine)
+        got, _ = engine.compute_batch(buf, offs, lens)
+        assert not _served_since(engine, t0, wait=0.01)
+        np.testing.assert_array_equal(got, np.array([o.icrc_of_frame(f) for f in fr[:10]], np.uint32))
+    finally:
+        engine.set_lanes(0)
+
+
 def test_service_off_is_the_launch_path(engine):
     engine.set_service(0)
     try:
