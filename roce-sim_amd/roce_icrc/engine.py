@@ -191,7 +191,13 @@ def _ptr(a) -> int | None:
     if isinstance(a, np.ndarray):
         if not a.flags.c_contiguous:
             raise ValueError("array must be C-contiguous")
-        return a.ctypes.data
+        # a writable buffer's address through ctypes.from_buffer costs a third
+        # of ndarray.ctypes (0.6 vs 1.7 us, five pointers per batch call: the
+        # per-call latency of small bursts is mostly this host side)
+        try:
+            return ctypes.addressof(ctypes.c_char.from_buffer(a))
+        except (TypeError, ValueError, BufferError):  # read-only or empty
+            return a.ctypes.data
     if hasattr(a, "data_ptr"):  # torch tensor (device-resident calls)
         return a.data_ptr()
     return int(a)
