@@ -1412,7 +1412,8 @@ __global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4
 // after `idle_ticks` of the 100 MHz real-time counter without a request:
 // every path through the loop reaches one of the two, so the grid always
 // drains; the host relaunches it on the next call.
-constexpr int kSvcThreads = 256;  // all stage the tables; wave 0 then serves
+constexpr int kSvcThreads = 512;  // all stage the tables; wave 0 serves, waves 1-7 help with bursts
+constexpr int kSvcWaves = kSvcThreads / 64;
 // LDS of the service (round 3): Mul(8192) for single frames (G = 64) and
 // Mul(1024) for bursts (G = 8) as the two halves of the Keys8 rows (64 KiB),
 // the combine sets Mul(-32), Mul(-128 2^l), l < 6 (both widths use the
@@ -1427,16 +1428,21 @@ constexpr uint32_t kSvcOut = kSvcLut + 256u - 16u;  // single frame: ICRC + stat
 constexpr uint32_t kBurstIcrc = kSvcLut + 256u;
 constexpr uint32_t kBurstOk = kBurstIcrc + 4u * kSvcMaxBurst;
 constexpr uint32_t kBurstSt = kBurstOk + kSvcMaxBurst;
-constexpr uint32_t kBurstStage = (kBurstSt + kSvcMaxBurst + 1023u) & ~1023u;
+// burst hand-off to the helper waves: generation, (count | verify << 31),
+// finished helpers, exit flag; then the burst's descriptors
+constexpr uint32_t kSvcCtl = kBurstSt + kSvcMaxBurst;
+constexpr uint32_t kSvcDescLds = kSvcCtl + 16u;
+constexpr uint32_t kBurstStage = (kSvcDescLds + 8u * kSvcMaxBurst + 1023u) & ~1023u;
 constexpr size_t kSvcLds = kBurstStage + kSvcMaxFrame + 1024u;  // (+ the last chunk's reach)
 static_assert(kSvcLds <= 163840, "service LDS");
 
-// One burst: frame i at stage + (desc[i] & 0xFFFFFFFF), length desc[i] >> 32,
-// eight frames at a time (G = 8 groups of the wave), folded from LDS.
+// One burst's share of wave `wave`: frame i at stage + (desc[i] & 0xFFFFFFFF),
+// length desc[i] >> 32 (descriptors in LDS), eight frames per round (G = 8
+// groups), rounds wave, wave + kSvcWaves, ... folded from LDS.
 template <bool VERIFY>
-__device__ __forceinline__ void serve_burst(const uint64_t* desc, uint32_t cnt, int lane) {
+__device__ __forceinline__ void serve_burst(uint32_t cnt, int lane, int wave) {
   constexpr int LOG2G = 3, G = 8, DPI = 4 * G;
-  const uint64_t dl = (uint32_t)lane < cnt ? desc[lane] : 0ull;  // every descriptor in one read
+  const uint64_t dl = *(const __attribute__((address_space(3))) uint64_t*)(uintptr_t)(kSvcDescLds + 8u * (uint32_t)lane);
   const uint32_t dlo = (uint32_t)dl, dhi = (uint32_t)(dl >> 32);
   const uint8_t* stage = (const uint8_t*)(__attribute__((address_space(3))) uint8_t*)(uintptr_t)kBurstStage;
   IcrcArgs a{};
@@ -1447,7 +1453,7 @@ __device__ __forceinline__ void serve_burst(const uint64_t* desc, uint32_t cnt, 
   a.status_out = (uint8_t*)(lds_u32*)(uintptr_t)kBurstSt;
   const int gl = lane & (G - 1), grp = lane >> LOG2G;
   const SvcKeysS kk = SvcKeysS::make(lane);
-  for (uint32_t s0 = 0; s0 < cnt; s0 += 64 / G) {
+  for (uint32_t s0 = (uint32_t)wave * (64 / G); s0 < cnt; s0 += kSvcWaves * (64 / G)) {
     const uint32_t i = s0 + (uint32_t)grp;
     const bool live = i < cnt;
     const uint32_t ii = live ? i : 0u;
@@ -1467,8 +1473,40 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   const int tid = threadIdx.x;
   stage_tables<LOG2G, kSvcThreads, SvcKeysL>(s.tables, tid);
   SvcKeysS::template stage<kSvcThreads>(s.tables + 3 * 1024, tid);  // main set 3: Mul(1024)
+  if (tid < 4) lds_wr(kSvcCtl + 4u * (uint32_t)tid, 0u);
   __syncthreads();
-  if (tid >= 64) return;
+  typedef __attribute__((address_space(3))) uint32_t lds_w;
+  auto ctl = [](uint32_t i) {  // (the helpers' spin reads must not be hoisted)
+    return __hip_atomic_load((lds_w*)(uintptr_t)(kSvcCtl + 4u * i), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  if (tid >= 64) {
+    // helper wave: each burst generation wave 0 posts, fold this wave's
+    // rounds, count itself done; leave when wave 0 leaves
+    const int wave = tid >> 6, hl = tid & 63;
+    uint32_t gen = 0;
+    for (;;) {
+      const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl(0));
+      if (g != gen) {
+        gen = g;
+        const uint32_t prm = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl(1));
+        const uint32_t cnt = min(prm & 0xFFu, kSvcMaxBurst);
+        if (prm >> 31)
+          serve_burst<true>(cnt, hl, wave);
+        else
+          serve_burst<false>(cnt, hl, wave);
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's results have landed
+        __asm__ __volatile__("" ::: "memory");
+        if (hl == 0)
+          __hip_atomic_fetch_add((lds_w*)(uintptr_t)(kSvcCtl + 8u), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        continue;
+      }
+      if (ctl(3) != 0u) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   const int lane = tid;
   const SvcKeysL kk = SvcKeysL::make(lane);
   ServiceRing* r = s.ring;
@@ -1496,19 +1534,45 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
         const uint32_t kib = min((L >> 16) & 0x7Fu, kSvcMaxFrame / 1024u);  // packed KiB
         const uint64_t* desc = (const uint64_t*)((const uint8_t*)r + kSvcDesc);
         // the packed frames into LDS: one LDS-DMA wave-instruction per KiB, all
-        // in flight at once (one PCIe round trip)
+        // in flight at once (one PCIe round trip), and every descriptor with
+        // one load
         for (uint32_t k = 0; k < kib; ++k)
           __builtin_amdgcn_global_load_lds(
               (const __attribute__((address_space(1))) void*)(frame + 1024u * k + 16u * (uint32_t)lane),
               (__attribute__((address_space(3))) void*)(uintptr_t)(kBurstStage + 1024u * k), 16, 0, 0);
+        const uint64_t dl = (uint32_t)lane < cnt ? desc[lane] : 0ull;
+        *(__attribute__((address_space(3))) uint64_t*)(uintptr_t)(kSvcDescLds + 8u * (uint32_t)lane) = dl;
         __asm__ __volatile__("" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the frames are in LDS
+        __builtin_amdgcn_s_waitcnt(0);  // frames and descriptors are in LDS
         __asm__ __volatile__("" ::: "memory");
         if (cnt > 0) {
+          // post the burst to the helper waves, take this wave's rounds
+          if (lane == 0) {
+            lds_wr(kSvcCtl + 4u, cnt | ((L & kSvcVerify) ? 0x80000000u : 0u));
+            __asm__ __volatile__("" ::: "memory");
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // (lgkmcnt(0): the parameters first)
+            __asm__ __volatile__("" ::: "memory");
+            __hip_atomic_store((lds_w*)(uintptr_t)kSvcCtl, ctl(0) + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
           if (L & kSvcVerify)
-            serve_burst<true>(desc, cnt, lane);
+            serve_burst<true>(cnt, lane, 0);
           else
-            serve_burst<false>(desc, cnt, lane);
+            serve_burst<false>(cnt, lane, 0);
+          // every helper counts itself done (those with no round at once);
+          // bounded: a burst not finished within 100 ms ends the service
+          // unanswered (the host then times out and takes the launch path)
+          const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+          bool helped = true;
+          while ((uint32_t)__builtin_amdgcn_readfirstlane((int)ctl(2)) < (uint32_t)(kSvcWaves - 1)) {
+            if (__builtin_amdgcn_s_memrealtime() - tw > 10000000ull) {
+              helped = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!helped) break;
+          if (lane == 0) lds_wr(kSvcCtl + 8u, 0u);
         }
         // the results (flat and LDS stores) have landed before the lanes read them
         __asm__ __volatile__("" ::: "memory");
@@ -1561,6 +1625,8 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
     if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) break;
     __builtin_amdgcn_s_sleep(2);
   }
+  if (lane == 0)  // the helper waves leave too
+    __hip_atomic_store((lds_w*)(uintptr_t)(kSvcCtl + 12u), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane == 0) __hip_atomic_store(&r->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
