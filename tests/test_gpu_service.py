@@ -236,6 +236,46 @@ def test_bursts_past_the_slot_take_the_launch_path(engine):
         engine.set_lanes(0)
 
 
+def test_services_of_several_threads(engine):
+    """The reference's gRPC side server calls from a 10-thread pool
+    (src/sanity_side.py:383): one context per thread, each with its own
+    resident workgroup; single frames and bursts from 4 threads at once stay
+    bit-exact."""
+    import threading
+    rng = np.random.default_rng(21)
+    frames = [o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x01, psn=i, dqpn=3),
+                            payload=rng.integers(0, 256, int(rng.integers(0, 3000)),
+                                                 dtype=np.uint8).tobytes()) for i in range(48)]
+    want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
+    errors = []
+
+    def worker(t):
+        try:
+            with IcrcEngine(0) as e:
+                r = np.random.default_rng(t)
+                for it in range(150):
+                    k = int(r.integers(1, 24))
+                    idx = r.choice(len(frames), k, replace=False)
+                    sel = [frames[i] for i in idx]
+                    if k == 1:
+                        got = np.array([e.compute_one(sel[0])[0]], np.uint32)
+                    else:
+                        got, _ = e.compute_batch(*_pack(sel, gap=int(r.integers(0, 3))))
+                    if not (got == want[idx]).all():
+                        errors.append((t, it))
+                        return
+        except Exception as ex:  # noqa: BLE001 (reported below)
+            errors.append((t, repr(ex)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=60)
+    assert not any(x.is_alive() for x in th), "a worker hung"
+    assert not errors, errors
+
+
 def test_service_off_is_the_launch_path(engine):
     engine.set_service(0)
     try:
