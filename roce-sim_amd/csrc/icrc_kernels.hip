@@ -458,9 +458,12 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
 
 // Tail stealing (strided kernel): the last 1/kTailDiv of a workgroup's sets
 // are claimed dynamically; a finished wave tries up to kMaxVictims other
-// workgroups' tails.
+// workgroups' tails.  Round 3, cfg2 kernel ms (3 A/B rounds each, two
+// sessions, profiles/r03q_tail_ab*.txt): 1/2 0.6417, 1/4 0.6309, 1/8
+// 0.6246 (+1.0 %), 1/16 0.6353, 1/32 0.6364; 2 victims at 1/8 0.6274, 8
+// victims at 1/4 0.6324.
 #ifndef RICRC_TAIL_DIV
-#define RICRC_TAIL_DIV 4
+#define RICRC_TAIL_DIV 8
 #endif
 constexpr uint32_t kTailDiv = RICRC_TAIL_DIV;
 #ifndef RICRC_MAX_VICTIMS
