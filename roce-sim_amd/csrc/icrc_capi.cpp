@@ -396,6 +396,7 @@ int seg_launch(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes, const ricrc
   a.icrc_out = d_icrc;
   a.status_out = d_status;
   a.tables = c->d_tables;
+  if (c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
   service_pause(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(ricrc::launch_segment(a, seg_log2g(c, pmtu), c->num_cus, s));

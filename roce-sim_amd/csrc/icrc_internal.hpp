@@ -79,6 +79,8 @@ struct SegArgs {
   uint32_t* icrc_out;   // nullable
   uint8_t* status_out;  // nullable
   const uint32_t* tables;
+  unsigned long long* claims;  // tail-claim counters (nullable: static ranges only)
+  uint32_t epoch;
 };
 
 // Enqueues the packet -> WR map kernel and the segmentation kernel.

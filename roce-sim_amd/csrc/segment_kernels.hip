@@ -58,6 +58,14 @@ __device__ __forceinline__ u32x4 ldmr(const uint8_t* p) {
 #define RICRC_SEG_THREADS 512  // 8 waves x ~200 VGPRs: no spills (16 waves spill ~20 VGPRs)
 #endif
 constexpr int kSegUnroll = RICRC_SEG_UNROLL;  // body iterations (16-byte MR loads per lane) in flight
+#ifndef RICRC_SEG_TAIL_DIV
+#define RICRC_SEG_TAIL_DIV 4
+#endif
+// last 1/kSegTailDiv of a range claimed dynamically: seg kernel ms (3 A/B
+// rounds, profiles/r03q_seg_tail_ab.txt) static 1.692-1.723, 1/4
+// 1.660-1.691 (+1.8 %), 1/8 1.661-1.701, 1/16 1.692-1.693
+constexpr uint32_t kSegTailDiv = RICRC_SEG_TAIL_DIV;
+constexpr uint32_t kSegMaxVictims = 4;
 constexpr int kSegThreads = RICRC_SEG_THREADS;  // one workgroup per CU (the tables fill the LDS)
 constexpr int kSegWaves = kSegThreads / 64;
 // Cache policy of the frame stores (stg128 in icrc_device.hpp; 2 = nt).
@@ -349,10 +357,24 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
   const uint8_t* mr_hi = a.mr_bytes >= 16 ? mr_end - 16 : a.mr;
   const uint32_t nsets = (a.npkts + PPW - 1) / PPW;
   const uint32_t per_block = (nsets + gridDim.x - 1) / gridDim.x;
-  const uint32_t set_begin = blockIdx.x * per_block;
-  const uint32_t set_end = min(nsets, set_begin + per_block);
+  // A workgroup's range [begin, end) of sets; its last 1/kSegTailDiv is
+  // claimed set by set through the workgroup's counter, from which the
+  // workgroups that finish first also claim (the strided ICRC kernel's tail
+  // stealing, icrc_kernels.hip; a packet's frame slot and outputs do not
+  // depend on who builds it).
+  auto range = [&](uint32_t blk, uint32_t& b, uint32_t& e, uint32_t& split) {
+    b = blk * per_block;
+    e = min(nsets, b + per_block);
+    const uint32_t len = b < e ? e - b : 0u;
+    split = e - (a.claims ? len / kSegTailDiv : 0u);
+  };
+  uint32_t set_begin, set_end, set_split;
+  range(blockIdx.x, set_begin, set_end, set_split);
+  unsigned long long* claims =
+      a.claims ? a.claims + (size_t)(a.epoch % kClaimSlots) * kMaxClaimBlocks : nullptr;
+  if (claims && tid == 0) atomicExch(&claims[blockIdx.x], (unsigned long long)a.epoch << 32);
 
-  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_end; set += (uint32_t)kSegWaves) {
+  auto do_set = [&](uint32_t set) {
     const uint32_t pkt = set * PPW + grp;
     uint32_t status;
     const Seg s = describe_seg(a, pkt, pkt < a.npkts, status, mr_hi);
@@ -529,6 +551,29 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
       a.lens[pkt] = s.live ? 4u * (uint32_t)s.T : 0u;
       if (a.icrc_out) a.icrc_out[pkt] = s.live ? icrc : 0u;
       if (a.status_out) a.status_out[pkt] = (uint8_t)status;
+    }
+  };
+  for (uint32_t set = set_begin + (uint32_t)(tid >> 6); set < set_split; set += (uint32_t)kSegWaves)
+    do_set(set);
+  if (claims) {  // own tail, then up to kMaxVictims other workgroups' tails
+    uint32_t victim = blockIdx.x, tries = 0;
+    auto claim = [&](uint32_t v) -> uint32_t {  // set index, or ~0u if v's tail is empty
+      unsigned long long old = 0;
+      if (lane == 0) old = atomicAdd(&claims[v], 1ull);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)old);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(old >> 32));
+      uint32_t vb, ve, vs;
+      range(v, vb, ve, vs);
+      return (hi == a.epoch && lo < ve - vs) ? vs + lo : ~0u;
+    };
+    for (;;) {
+      const uint32_t cur = claim(victim);
+      if (cur == ~0u) {
+        if (++tries > kSegMaxVictims) break;
+        victim = (blockIdx.x + 2 * tries - 1) % gridDim.x;
+        continue;
+      }
+      do_set(cur);
     }
   }
 }
