@@ -216,6 +216,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   a.tables = c->d_tables;
   HIP_TRY(hipSetDevice(c->device));
   if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0) {
+    if (c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
     HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
   } else {
     if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);

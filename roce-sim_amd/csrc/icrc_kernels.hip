@@ -1072,6 +1072,13 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 #define RICRC_SMALL_WAVES 12
 #endif
 constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
+// Tail stealing (below): cfg5 kernel ms, 6 A/B rounds over two sessions
+// (profiles/r03q_small_tail_ab*.txt): static 0.3132-0.3161, 1/4 0.3139-0.3175,
+// 1/8 0.3115-0.3122, 1/16 0.3106-0.3148 (+0.9 % mean), 1/32 0.3122-0.3135.
+#ifndef RICRC_SMALL_TAIL_DIV
+#define RICRC_SMALL_TAIL_DIV 16
+#endif
+constexpr uint32_t kSmallTailDiv = RICRC_SMALL_TAIL_DIV;
 using SmallKeys = Keys8;
 constexpr uint32_t kSmallComb = 163840u - 4096u;
 constexpr uint32_t kSmallStage = 65536;
@@ -1233,17 +1240,30 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   // the prefetch two rounds past its end re-reads the range's last batch
   // (still in L2) instead of the next workgroup's first ones, which that
   // workgroup reads again much later (an extra ~2.3 % of HBM reads at cfg5).
-  const uint32_t bs_end = min(b1, last);
+  //
+  // Tail stealing (as in the strided kernel): the last 1/kSmallTailDiv of a
+  // workgroup's staged batches [split, end) are claimed batch by batch
+  // through its counter, by its own waves and by workgroups that are done;
+  // their words go straight to icrc_out.  The ring covers [b0, split).
+  auto range = [&](uint32_t blk, uint32_t& rb, uint32_t& re, uint32_t& rs) {
+    rb = blk * per_block;
+    re = min(min(nb, rb + per_block), last);
+    const uint32_t len = rb < re ? re - rb : 0u;
+    rs = re - (a.claims ? len / kSmallTailDiv : 0u);
+  };
+  uint32_t rb_, re_, bs_end;
+  range(blockIdx.x, rb_, re_, bs_end);
+  unsigned long long* claims =
+      a.claims ? a.claims + (size_t)(a.epoch % kClaimSlots) * kMaxClaimBlocks : nullptr;
+  if (claims && tid == 0) atomicExch(&claims[blockIdx.x], (unsigned long long)a.epoch << 32);
+  uint32_t lim = bs_end > 0 ? bs_end - 1u : 0u;  // prefetch clamp (no clamp while claiming)
   auto load = [&](uint32_t b, u32x4* Rg) {  // unconditional: clamped chunk index
-#ifdef RICRC_SMALL_OLD_CLAMP  // A/B switch: round-2 clamp (prefetch reaches the next range)
-    const uint8_t* base = a.frames + (uint64_t)min(b, last - 1) * 64u * S;
-#else
-    const uint8_t* base = a.frames + (uint64_t)min(b, bs_end - 1u) * 64u * S;
-#endif
+    const uint8_t* base = a.frames + (uint64_t)min(b, lim) * 64u * S;
 #pragma unroll
     for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
   };
-  auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext, bool live = true) {
+  auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext, bool live = true,
+                            bool to_ring = true) {  // (to the ring when there is one)
 #ifdef RICRC_SMALL_ABLATE_STAGE  // diagnostic build only: loads and output stores, no LDS, no fold
     {
       u32x4 acc = Rg[0];
@@ -1289,7 +1309,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     } else {
       R = small_fold_masked<false>(nullptr, pb, ihl, n);
     }
-    emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing);
+    emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing && to_ring);
     __asm__ __volatile__("" ::: "memory");
   };
 
@@ -1351,6 +1371,34 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       stage_and_fold(b + nw, Y, b + 3 * nw);
     }
     if (i < cnt) stage_and_fold(b, X, b + 2 * nw);
+  }
+  if (claims) {  // own tail, then up to kMaxVictims other workgroups' tails
+    lim = 0xFFFFFFFFu;
+    uint32_t victim = blockIdx.x, tries = 0;
+    auto claim = [&]() -> uint32_t {  // a batch, or ~0u when every tail tried is empty
+      for (;;) {
+        unsigned long long old = 0;
+        if (lane == 0) old = atomicAdd(&claims[victim], 1ull);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)old);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(old >> 32));
+        uint32_t vb, ve, vs;
+        range(victim, vb, ve, vs);
+        if (hi == a.epoch && vs < ve && lo < ve - vs) return vs + lo;
+        if (++tries > kMaxVictims) return ~0u;
+        victim = (blockIdx.x + 2 * tries - 1) % gridDim.x;
+      }
+    };
+    uint32_t cur = claim();
+    if (cur != ~0u) {
+      u32x4 X[C];
+      load(cur, X);
+      for (;;) {  // the next claim's loads go out while this batch folds
+        const uint32_t nxt = claim();
+        stage_and_fold(cur, X, nxt == ~0u ? cur : nxt, true, false);
+        if (nxt == ~0u) break;
+        cur = nxt;
+      }
+    }
   }
   // the last batch, straight from global memory (one wave of the owning block)
   if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % nw) {
