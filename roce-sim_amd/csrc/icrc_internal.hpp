@@ -132,6 +132,8 @@ constexpr uint32_t kSvcDesc = kSvcFrame + kSvcMaxFrame;
 constexpr uint32_t kSvcAns = kSvcDesc + 8 * kSvcMaxBurst;
 constexpr size_t kSvcBytes = kSvcAns + 8 * kSvcMaxBurst;
 static_assert(sizeof(ServiceRing) == 256, "two 128-byte lines");
+static_assert(offsetof(ServiceRing, req) == 0 && offsetof(ServiceRing, stop) == 8,
+              "the service polls req and stop with one 16-byte load");
 
 struct ServiceArgs {
   ServiceRing* ring;  // device view of the host slot

@@ -1571,10 +1571,15 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   a.icrc_out = (uint32_t*)(lds_u32*)(uintptr_t)kOut;
   a.status_out = (uint8_t*)(lds_u32*)(uintptr_t)(kOut + 4u);
   uint32_t served = s.served;
+  const auto ring_rsrc = out_rsrc(r, 16u);
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   uint32_t polls = 0;
   for (;; ++polls) {
-    const uint64_t req = __hip_atomic_load(&r->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // ONE PCIe read per poll: the request word and the stop flag share the
+    // slot's first 16 bytes (a 16-byte system-coherent load, sc0 sc1); two
+    // separate loads made every poll two round trips
+    const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, 0u, 0u, 17);
+    const uint64_t req = (uint64_t)head.x | ((uint64_t)head.y << 32);
     const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)req);
     if (seq != served) {
       const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
@@ -1672,7 +1677,7 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
       t_last = __builtin_amdgcn_s_memrealtime();
       continue;
     }
-    if (__hip_atomic_load(&r->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)head.z) != 0u) break;  // stop
     if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) break;
     __builtin_amdgcn_s_sleep(2);
   }
