@@ -477,11 +477,17 @@ class Segment:
     def lanes(self):
         return self.eng.lanes_for_len(self.slot - 192)
 
-    def frames_ok(self):
-        self.torch.cuda.synchronize()
-        fr = self.d_frames[: 64 * self.slot].cpu().numpy().reshape(64, self.slot)
-        lens = self.d_lens[:64].cpu().numpy()
-        return lambda p, f: lens[p] == len(f) and fr[p, : len(f)].tobytes() == f
+    def frames_ok(self, pk=None):
+        """Checker for the frames of packets `pk` (default: WR 0's): (i, frame)
+        -> packet pk[i]'s slot and length equal the oracle's frame."""
+        torch = self.torch
+        torch.cuda.synchronize()
+        if pk is None:
+            pk = np.arange(min(self.n, SEG_MSG // self.pmtu))
+        idx = torch.from_numpy(np.asarray(pk, np.int64)).to(self.d_frames.device)
+        fr = self.d_frames.view(self.n, self.slot).index_select(0, idx).cpu().numpy()
+        lens = self.d_lens.index_select(0, idx).cpu().numpy()
+        return lambda i, f: lens[i] == len(f) and fr[i, : len(f)].tobytes() == f
 
     def check(self):
         from roce_icrc import engine as E
@@ -504,22 +510,31 @@ def parity_leg(W, gpu_icrc: np.ndarray, seed: int) -> dict:
     """This rank's GPU ICRC words against the oracle's per-packet restatement
     of BTH.compute_icrc (src/roce.py:192-223) on a seeded sample of its
     packets (all of them when there are fewer than PARITY_SAMPLE); for
-    segmentation, the frames and words of the first WR against
-    segment_oracle.  Oracle use is confined to this checker."""
+    segmentation, the whole frames and words of a seeded sample of WRs
+    (PARITY_SAMPLE packets' worth) against segment_oracle.  Oracle use is
+    confined to this checker."""
     sys.path.insert(0, str(ROOT / "oracle"))
     t0 = time.perf_counter()
     if isinstance(W, Segment):
         import segment_oracle as so
-        ok = W.frames_ok()
-        r = W.rec[0]
-        wr = so.SegWR(op=int(r["op"]), mr_offset=int(r["mr_offset"]), length=int(r["length"]),
-                      psn=int(r["psn"]), dqpn=int(r["dqpn"]), src_ip=int(r["src_ip"]),
-                      dst_ip=int(r["dst_ip"]), sport=int(r["sport"]), flags=int(r["flags"]),
-                      imm=int(r["imm"]))
-        want = so.segment(memoryview(W.mr), [wr], W.pmtu)
-        mism = sum(int(not ok(p, f)) for p, f in enumerate(want))
-        mism += sum(int(gpu_icrc[p]) != int.from_bytes(f[-4:], "little") for p, f in enumerate(want))
-        return {"sampled": len(want), "mismatches": mism, "what": "frames + ICRC words of WR 0",
+        per = SEG_MSG // W.pmtu
+        nwr = W.rec.size
+        kw = min(nwr, max(1, PARITY_SAMPLE // per))
+        widx = (np.sort(np.random.default_rng(seed).choice(nwr, size=kw, replace=False)) if kw < nwr
+                else np.arange(nwr))
+        # the plan packs WR w's packets at w * per (equal-length WRs)
+        pk = (widx[:, None] * per + np.arange(per)[None, :]).reshape(-1)
+        ok = W.frames_ok(pk)
+        wrs = [so.SegWR(op=int(r["op"]), mr_offset=int(r["mr_offset"]), length=int(r["length"]),
+                        psn=int(r["psn"]), dqpn=int(r["dqpn"]), src_ip=int(r["src_ip"]),
+                        dst_ip=int(r["dst_ip"]), sport=int(r["sport"]), flags=int(r["flags"]),
+                        imm=int(r["imm"])) for r in W.rec[widx]]
+        want = so.segment(memoryview(W.mr), wrs, W.pmtu)
+        assert len(want) == pk.size
+        mism = sum(int(not ok(i, f)) for i, f in enumerate(want))
+        mism += sum(int(gpu_icrc[p]) != int.from_bytes(f[-4:], "little") for p, f in zip(pk, want))
+        return {"sampled": len(want), "mismatches": mism,
+                "what": f"whole frames + ICRC words of {kw} seeded WRs",
                 "s": round(time.perf_counter() - t0, 2)}
     import icrc_oracle as orc
     n = gpu_icrc.size
