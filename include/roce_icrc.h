@@ -5,7 +5,7 @@
  *
  *   reference                                   replaced by
  *   ------------------------------------------  ---------------------------------
- *   BTH.compute_icrc(self, p)  src/roce.py:192   ricrc_compute_one / ricrc_compute_batch
+ *   BTH.compute_icrc(self, p)  src/roce.py:192   ricrc_icrc / ricrc_compute_one / ricrc_compute_batch
  *     (fires from BTH.post_build src/roce.py:228-233, itself run by scapy
  *      send() at src/roce_sq.py:1197 (requester emit, retry re-emit via
  *      src/roce_sq.py:743) and src/roce_rq.py:731 (responder emit))
@@ -39,7 +39,8 @@
  * Threading.  All entry points are re-entrant.  A ricrc_ctx owns one HIP
  * stream plus device scratch and is NOT thread-safe: use one context per host
  * thread (the reference calls from a 10-thread gRPC pool,
- * src/sanity_side.py:383).  Python's ctypes releases the GIL around calls.
+ * src/sanity_side.py:383), or the context-free ricrc_icrc, which is
+ * thread-safe.  Python's ctypes releases the GIL around calls.
  *
  * Return codes: 0 on success, a negative errno-style code otherwise.
  */
@@ -106,6 +107,15 @@ void* ricrc_ctx_stream(ricrc_ctx* ctx);
  * service is off, take one staged kernel launch per call instead. */
 int ricrc_compute_one(ricrc_ctx* ctx, const uint8_t* frame, size_t len, uint32_t* icrc_out,
                       uint8_t* status_out /* nullable */);
+/* The same per-packet drop-in without a context, thread-safe: what a
+ * `compute_icrc` hook (src/roce.py:192) called from any thread of the
+ * reference's gRPC pool (src/sanity_side.py:383) binds to.  Each calling
+ * thread borrows one library-owned context on its current HIP device (created
+ * on the thread's first call, ~ms); a thread that exits returns it to a pool
+ * that later threads reuse, and the pool lives until process exit.  Same
+ * answers, status bits and costs as ricrc_compute_one. */
+int ricrc_icrc(const uint8_t* frame, size_t len, uint32_t* icrc_out,
+               uint8_t* status_out /* nullable */);
 /* Idle timeout of the per-packet service in microseconds (default 1000);
  * 0 turns the service off (ricrc_compute_one and small bursts then launch a
  * kernel per call). */

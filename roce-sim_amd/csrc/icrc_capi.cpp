@@ -602,6 +602,50 @@ int service_burst(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offsets,
   return RICRC_OK;
 }
 
+// ---- context-free per-packet call (ricrc_icrc) -----------------------------
+// A context is single-threaded, so each calling thread borrows one
+// library-owned context per device.  A thread that exits hands its contexts
+// back to a pool for the next thread (a gRPC pool's churn creates no more
+// contexts than threads ever ran at once); pooled contexts live until process
+// exit, where service_atexit stops their waves -- no HIP call runs on the
+// thread-exit path.
+std::mutex g_pool_mu;
+std::vector<ricrc_ctx*> g_pool;
+
+struct ThreadContexts {
+  std::vector<ricrc_ctx*> ctxs;
+  ~ThreadContexts() {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (ricrc_ctx* c : ctxs) g_pool.push_back(c);
+  }
+};
+
+int thread_ctx(int device, ricrc_ctx** out) {
+  static thread_local ThreadContexts t;
+  for (ricrc_ctx* c : t.ctxs)
+    if (c->device == device) {
+      *out = c;
+      return RICRC_OK;
+    }
+  ricrc_ctx* c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i)
+      if (g_pool[i]->device == device) {
+        c = g_pool[i];
+        g_pool.erase(g_pool.begin() + (long)i);
+        break;
+      }
+  }
+  if (!c) {
+    const int rc = ricrc_ctx_create(device, &c);
+    if (rc != RICRC_OK) return rc;
+  }
+  t.ctxs.push_back(c);
+  *out = c;
+  return RICRC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -732,6 +776,16 @@ int ricrc_compute_one(ricrc_ctx* c, const uint8_t* frame, size_t len, uint32_t* 
   const uint64_t off = 0;
   const uint32_t l = (uint32_t)len;
   return host_ragged(c, frame, len, &off, &l, 1, icrc_out, status_out, nullptr, false);
+}
+
+int ricrc_icrc(const uint8_t* frame, size_t len, uint32_t* icrc_out, uint8_t* status_out) {
+  if (!frame || !icrc_out || len > 0xFFFFFFFFull) return RICRC_EINVAL;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return RICRC_ENODEV;
+  ricrc_ctx* c = nullptr;
+  const int rc = thread_ctx(dev, &c);
+  if (rc != RICRC_OK) return rc;
+  return ricrc_compute_one(c, frame, len, icrc_out, status_out);
 }
 
 int ricrc_compute_batch(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,

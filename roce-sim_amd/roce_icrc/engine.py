@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import threading
 from pathlib import Path
 
 import numpy as np
@@ -82,6 +83,7 @@ _SIGNATURES = {
     "ricrc_ctx_set_service": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "ricrc_ctx_service_times": (ctypes.c_int, [_vp, _vp]),
     "ricrc_compute_one": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, _vp]),
+    "ricrc_icrc": (ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp]),
     "ricrc_compute_batch": (
         ctypes.c_int,
         [_vp, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_uint32, _vp, _vp],
@@ -236,6 +238,31 @@ def _u8(a) -> np.ndarray:
     if a.dtype != np.uint8:
         a = a.view(np.uint8)
     return a
+
+
+_tls = threading.local()  # per-thread ctypes outputs of icrc()
+
+
+def icrc(frame) -> tuple[int, int]:
+    """Context-free, thread-safe drop-in for BTH.compute_icrc (src/roce.py:192):
+    wire frame -> (icrc, status) through ricrc_icrc, which serves each calling
+    thread from a library-owned context on the thread's current HIP device
+    (the reference calls compute_icrc from a 10-thread gRPC pool,
+    src/sanity_side.py:383)."""
+    lib = load_library()
+    o = getattr(_tls, "out", None)
+    if o is None:
+        o = _tls.out = (ctypes.c_uint32(0), ctypes.c_uint8(0))
+        _tls.refs = (ctypes.byref(o[0]), ctypes.byref(o[1]))
+    if isinstance(frame, bytes):
+        ptr, n = frame, len(frame)
+    else:
+        f = _u8(frame)
+        ptr, n = (_ptr(f) if f.size else b""), f.size
+    rc = lib.ricrc_icrc(ptr, n, *_tls.refs)
+    if rc != RICRC_OK:
+        raise IcrcError("ricrc_icrc", rc, lib.ricrc_strerror(rc).decode())
+    return o[0].value, o[1].value
 
 
 class IcrcEngine:

@@ -2,7 +2,8 @@
  * cgo / JNI / N-API binding of include/roce_icrc.h sees.  ricrc_compute_one
  * (the per-packet drop-in of BTH.compute_icrc, src/roce.py:192) and small
  * ricrc_compute_batch bursts, with the resident service and with one kernel
- * launch per call; every service answer is compared with the launch path's.
+ * launch per call, and the context-free ricrc_icrc; every service answer is
+ * compared with the launch path's.
  *
  * build (from the repo root, after make -C roce-sim_amd):
  *   gcc -std=c99 -O2 -Iinclude scripts/latency_c.c -Lroce-sim_amd/roce_icrc \
@@ -120,6 +121,23 @@ int main(void) {
       }
       report("compute_batch", n == 64 ? "ACK (48 B)" : "mixed-MTU", n, svcs[si], t);
     }
+  }
+  /* the context-free call (a library-owned context of this thread) */
+  for (int k = 0; k < 3; ++k) {
+    make_frame(buf, sizes[k], 7u + k);
+    uint32_t want = 0;
+    ricrc_ctx_set_service(ctx, 0);
+    ricrc_compute_one(ctx, buf, sizes[k], &want, NULL);
+    for (int w = 0; w < 50; ++w) ricrc_icrc(buf, sizes[k], out, st);
+    for (int r = 0; r < REPS; ++r) {
+      const double t0 = now_us();
+      ricrc_icrc(buf, sizes[k], out, st);
+      t[r] = now_us() - t0;
+      bad += out[0] != want;
+    }
+    char what[32];
+    snprintf(what, sizeof what, "%u B", sizes[k]);
+    report("icrc", what, 1, 1000, t);
   }
   ricrc_ctx_destroy(ctx);
   printf("{\"mismatches_vs_launch_path\": %d}\n", bad);

@@ -1,7 +1,8 @@
 /* A plain C99 consumer of include/roce_icrc.h: proves the header is valid C
  * and the library links without C++ or HIP headers on the caller's side.
  * Without a GPU it runs planning and argument checks only; with one it also
- * drives the GPU path through the C ABI (per-packet drop-in, a ragged batch
+ * drives the GPU path through the C ABI (per-packet drop-in with and without
+ * a context, a ragged batch
  * in compute and verify mode, and -- with two or more devices -- the
  * round-robin multi-device split).  Prints one line; exit status != 0 names
  * the failed check. */
@@ -23,6 +24,10 @@ static int gpu_leg(ricrc_ctx* ctx, int ndev) {
   uint8_t st = 0xFF;
   if (ricrc_compute_one(ctx, kFrame, sizeof kFrame, &icrc, &st) != RICRC_OK) return 20;
   if (icrc != kIcrc || st != 0) return 21;
+  icrc = 0;
+  st = 0xFF;
+  if (ricrc_icrc(kFrame, sizeof kFrame, &icrc, &st) != RICRC_OK) return 29;  /* no context */
+  if (icrc != kIcrc || st != 0) return 30;
   /* a ragged batch: the frame, a copy with one payload bit flipped, the frame
    * again at an offset 4 bytes further */
   uint8_t buf[160];
@@ -73,6 +78,10 @@ int main(void) {
   int ndev = -1;
   if (ricrc_device_count(&ndev) != RICRC_OK) return 6;
   if (ndev == 0 && (rc != RICRC_ENODEV || ctx != NULL)) return 7;
+  if (ndev == 0) {
+    uint32_t icrc = 0;
+    if (ricrc_icrc(kFrame, sizeof kFrame, &icrc, NULL) != RICRC_ENODEV) return 8;
+  }
   int gpu = -1;
   if (ctx) {
     gpu = gpu_leg(ctx, ndev);

@@ -29,6 +29,7 @@ def test_null_arguments_rejected_without_touching_a_device():
     lib = E.load_library()
     assert lib.ricrc_ctx_create(0, None) == -22
     assert lib.ricrc_compute_one(None, None, 0, None, None) == -22
+    assert lib.ricrc_icrc(None, 0, None, None) == -22
     assert lib.ricrc_compute_batch_multi(None, 0, None, 0, None, None, 0, None, None) == -22
     assert lib.ricrc_ctx_set_lanes_per_packet(None, 8) == -22
 
@@ -40,6 +41,10 @@ def test_no_gpu_means_no_engine():
     assert E.device_count() == 0
     with pytest.raises(E.IcrcUnavailable):
         E.IcrcEngine(0)
+    # the context-free call finds no device either (no CPU fallback)
+    with pytest.raises(E.IcrcError) as ei:
+        E.icrc(b"\x45" + bytes(59))
+    assert ei.value.code == -19
 
 
 def test_product_package_never_imports_the_oracle():

@@ -310,3 +310,55 @@ def test_process_exit_with_the_wave_resident():
     assert r.returncode == 0, r.stderr[-2000:]
     assert "answered" in r.stdout
     assert time.perf_counter() - t0 < 60
+
+
+def test_context_free_icrc_every_frame_shape():
+    """ricrc_icrc (no context argument) gives compute_one's answers."""
+    from roce_icrc import engine as E
+    for f in _frames():
+        icrc, st = E.icrc(f)
+        assert icrc == _want(f), (len(f), hex(icrc), st)
+    assert E.icrc(b"")[1] & E.PKT_BAD_LEN
+
+
+def test_context_free_icrc_from_thread_pools():
+    """The reference's side server calls from ThreadPoolExecutor(max_workers=10)
+    (src/sanity_side.py:383): three pools one after another (their threads
+    exit, later threads take over the pooled contexts), every answer
+    bit-exact."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from roce_icrc import engine as E
+    rng = np.random.default_rng(31)
+    frames = [o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x01, psn=i, dqpn=3),
+                            payload=rng.integers(0, 256, int(rng.integers(0, 4097)),
+                                                 dtype=np.uint8).tobytes()) for i in range(64)]
+    want = [o.icrc_of_frame(f) for f in frames]
+    for rnd in range(3):
+        with ThreadPoolExecutor(max_workers=10) as ex:
+            got = list(ex.map(lambda i: E.icrc(frames[i % 64])[0], range(2000)))
+        bad = [i for i, g in enumerate(got) if g != want[i % 64]]
+        assert not bad, (rnd, bad[:5])
+
+
+def test_process_exit_after_context_free_calls_on_threads():
+    """Threads that used ricrc_icrc exit (their contexts go to the pool with
+    the waves still resident), then the process ends without any cleanup
+    call: the exit handler stops every wave."""
+    code = (
+        "import sys, threading; sys.path[:0] = [%r, %r]\n"
+        "from roce_icrc import engine as E\n"
+        "import icrc_oracle as o\n"
+        "f = o.sim_send_success_frame()\n"
+        "r = []\n"
+        "th = [threading.Thread(target=lambda: r.append(E.icrc(f)[0])) for _ in range(4)]\n"
+        "[t.start() for t in th]; [t.join() for t in th]\n"
+        "r.append(E.icrc(f)[0])\n"
+        "assert r == [0x1BE21D75] * 5, r\n"
+        "print('answered', flush=True)\n"
+        % (str(ROOT / "roce-sim_amd"), str(ROOT / "oracle")))
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "answered" in r.stdout
+    assert time.perf_counter() - t0 < 60
