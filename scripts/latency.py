@@ -67,6 +67,18 @@ def main():
             eng.compute_one(frame)
             print(json.dumps({"call": "compute_one after idle exit", "frame_bytes": flen,
                               "us": round((time.perf_counter() - t0) * 1e6, 1)}), flush=True)
+    # the context-free call (engine.icrc -> ricrc_icrc, this thread's
+    # library-owned context)
+    from roce_icrc import engine as E
+    for pay in (0, 4096):
+        buf, stride, flen = synth.uniform_frames(1, pay)
+        frame = bytes(buf[:flen])
+        want = orc.icrc_of_frame(frame)
+        got = []
+        med, p99 = med_us(lambda: got.append(E.icrc(frame)[0]), a.reps)
+        assert set(got) == {want}, (hex(want), {hex(x) for x in got})
+        print(json.dumps({"call": "icrc (no context)", "frame_bytes": flen,
+                          "median_us": round(med, 2), "p99_us": round(p99, 2)}), flush=True)
     # bursts: up to 64 frames / 64 KiB go to the resident wave as ONE request
     # (round 3), larger batches and service 0 launch the kernels
     acks = [orc.build_frame("10.0.0.2", "10.0.0.1", 9, dict(opcode=0x11, psn=i, dqpn=5),
