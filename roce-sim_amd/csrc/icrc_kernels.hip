@@ -1574,11 +1574,8 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   const auto ring_rsrc = out_rsrc(r, 16u);
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   uint32_t polls = 0;
-  for (;; ++polls) {
-    // ONE PCIe read per poll: the request word and the stop flag share the
-    // slot's first 16 bytes (a 16-byte system-coherent load, sc0 sc1); two
-    // separate loads made every poll two round trips
-    const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, 0u, 0u, 17);
+  // one poll's value: 0 = nothing to do, 1 = a request served, 2 = leave
+  auto step = [&](const u32x4 head) -> int {
     const uint64_t req = (uint64_t)head.x | ((uint64_t)head.y << 32);
     const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)req);
     if (seq != served) {
@@ -1627,7 +1624,7 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
             }
             __builtin_amdgcn_s_sleep(1);
           }
-          if (!helped) break;
+          if (!helped) return 2;
           if (lane == 0) lds_wr(kSvcCtl + 8u, 0u);
         }
         // the results (flat and LDS stores) have landed before the lanes read them
@@ -1652,7 +1649,7 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
         polls = 0;
         served = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
-        continue;
+        return 1;
       }
       const Pkt p = describe<DPI>(frame, 0, true, 0, L <= kSvcMaxFrame ? L : 0u);
       Batch<kUnroll> b = issue_packet<LOG2G, false>(p, lane);
@@ -1675,12 +1672,30 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
       polls = 0;
       served = seq;
       t_last = __builtin_amdgcn_s_memrealtime();
-      continue;
+      return 1;
     }
-    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)head.z) != 0u) break;  // stop
-    if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) break;
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)head.z) != 0u) return 2;  // stop
+    if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) return 2;
     __builtin_amdgcn_s_sleep(2);
+    return 0;
+  };
+  // ONE PCIe read per poll: the request word and the stop flag share the
+  // slot's first 16 bytes (a 16-byte system-coherent load, sc0 sc1; two
+  // separate loads made every poll two round trips), and TWO polls in
+  // flight: the next one is issued before this one's value is looked at, so
+  // a request is seen about half a round trip sooner.  A poll issued before a
+  // request was served shows its sequence number again (== served): ignored.
+  auto poll = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, 0u, 0u, 17); };
+  u32x4 hA = poll();
+  for (;;) {
+    const u32x4 hB = poll();
+    ++polls;
+    if (step(hA) == 2) break;
+    hA = poll();
+    ++polls;
+    if (step(hB) == 2) break;
   }
+  __builtin_amdgcn_s_waitcnt(0);  // the poll still in flight has returned
   if (lane == 0)  // the helper waves leave too
     __hip_atomic_store((lds_w*)(uintptr_t)(kSvcCtl + 12u), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
