@@ -4,8 +4,10 @@
 One step = one launch of the HIP ICRC kernel over one batch of synthetic frames
 already resident in HBM.  Default workload (N=1): BASELINE config 2, 2^20 RC
 SEND_MIDDLE frames with 4 KiB payloads (4140-B wire frames, compute mode).
-With --gpus N (one process per GPU via torch.distributed.run) the default
-workload is BASELINE config 4: ONE stream of 2^20 N frames (seed 0x1C2C0004,
+With --gpus N (one process per GPU: under torch.distributed.run, or -- run
+plainly as `python bench.py --gpus N` -- bench.py starts the N ranks itself
+under torch.distributed.run as a child process) the default workload is
+BASELINE config 4: ONE stream of 2^20 N frames (seed 0x1C2C0004,
 2^23 packets at N = 8), packet i on rank i mod N; there is no data-path
 collective, only a gloo barrier, a max-reduce of the timing (weak scaling) and
 a gather of every rank's parity result.  --workload cfg3 / cfg5 run the other
@@ -26,7 +28,8 @@ Printed (rank 0): ONE JSON line with the driver's keys plus
                    on; another build gives traffic null and says why);
   cpu_baseline  -- the per-packet Python restatement of BTH.compute_icrc
                    (datenlord/roce-sim src/roce.py:192-223, zlib.crc32), timed
-                   on this host's cores over a bounded sample (rank 0, N=1);
+                   on this host's cores over a bounded sample (rank 0, over
+                   its own shard at N > 1);
   parity        -- per-rank sampled bit-exactness against that restatement.
 """
 from __future__ import annotations
@@ -616,20 +619,52 @@ def enqueue_ceiling(torch, eng, W, stream, sp, dev):
     return result
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run WITHOUT a launcher (no WORLD_SIZE in the
+    environment): start the N ranks under torch.distributed.run as a child
+    process -- one process per GPU, 127.0.0.1 rendezvous -- and return its exit
+    status.  Called before anything touches torch or the GPU (the parent never
+    initialises a device, and never execs: the child is a separate process).
+    Rank 0 of the child prints the JSON line on the inherited stdout."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), str(Path(__file__).resolve()), *sys.argv[1:]]
+    print(f"[bench] --gpus {n} without a launcher: starting {n} ranks under "
+          "torch.distributed.run", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env, cwd=str(ROOT))
+
+
 def main():
     args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        # a launcher that started a different number of ranks than --gpus asks
+        # for would print a line for the wrong N: refuse
+        print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    if args.gpus != world and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
-              file=sys.stderr)
     # ROCE_ICRC_BENCH_DEVICE pins every rank to one device: a rehearsal of the
     # N-rank path on a 1-GPU box (never set by the driver's scaling runs)
     local = int(os.environ.get("ROCE_ICRC_BENCH_DEVICE", local))
@@ -739,12 +774,17 @@ def main():
         e2e = world * W.covered / min(ts) / 2**30
         del h_pinned, h_out
 
+    # CPU baseline (after every timed leg): rank 0 over its own frames -- at
+    # N > 1 its shard of the one cfg4 stream -- while the other ranks wait at
+    # the closing barrier, so the host pool has the node's cores to itself
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         if isinstance(W, Segment):
             cpu = cpu_baseline_seg(W.mr, W.rec, W.pmtu, W.frames_ok())
         else:
             cpu = cpu_baseline(W.buf, W.offs, W.lens, gpu_icrc)
+        if world > 1:
+            cpu["sample"] = f"rank 0's shard ({n} packets of {n * world}): " + cpu["sample"]
 
     if rank == 0:
         mean_k = float(np.mean(kern_s))

@@ -62,6 +62,8 @@ struct ricrc_ctx {
   hipStream_t svc_stream = nullptr;
   bool svc_launched = false;
   uint32_t svc_seq = 0;
+  uint32_t svc_served = 0;  // last request answered (or abandoned): the wave's start point
+  uint64_t* busy = nullptr;  // the device's service busy word (device_busy), once any service ran
   uint32_t svc_idle_us = 1000;  // 0 = service off (staged launch per call)
   std::chrono::steady_clock::time_point svc_last{};  // last call (the wave's idle clock)
 };
@@ -85,6 +87,39 @@ hipError_t prepare_device(int device) {
 }
 
 int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? RICRC_ENOMEM : RICRC_EIO; }
+
+// Per-device service busy word (ricrc::announce_batch): one host-mapped line
+// per device, allocated by the first per-packet service on that device and
+// kept until process exit.  Every batch launch on the device passes it to its
+// kernel, whichever context launches, so resident service waves of OTHER
+// contexts (ricrc_icrc's per-thread contexts, a gRPC pool's threads) leave
+// the CUs a starting batch needs.  Before any service ran on a device the
+// launches pass nullptr (nothing to announce to).
+constexpr int kMaxDevices = 64;
+std::atomic<uint64_t*> g_busy[kMaxDevices];
+std::mutex g_busy_mu;
+
+uint64_t* device_busy(int device) {
+  return (device >= 0 && device < kMaxDevices) ? g_busy[device].load(std::memory_order_acquire)
+                                                : nullptr;
+}
+
+hipError_t device_busy_init(int device, uint64_t** out) {
+  *out = device_busy(device);
+  if (*out || device < 0 || device >= kMaxDevices) return hipSuccess;
+  std::lock_guard<std::mutex> lk(g_busy_mu);
+  uint64_t* b = g_busy[device].load(std::memory_order_acquire);
+  if (!b) {
+    void* h = nullptr;
+    hipError_t e = hipHostMalloc(&h, ricrc::kBusyBytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    std::memset(h, 0, ricrc::kBusyBytes);
+    b = (uint64_t*)h;
+    g_busy[device].store(b, std::memory_order_release);
+  }
+  *out = b;
+  return hipSuccess;
+}
 
 #define HIP_TRY(expr)                          \
   do {                                         \
@@ -214,6 +249,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   a.status_out = status;
   a.ok_out = ok;
   a.tables = c->d_tables;
+  a.busy = device_busy(c->device);
   HIP_TRY(hipSetDevice(c->device));
   if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0) {
     if (c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
@@ -397,6 +433,7 @@ int seg_launch(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes, const ricrc
   a.icrc_out = d_icrc;
   a.status_out = d_status;
   a.tables = c->d_tables;
+  a.busy = device_busy(c->device);
   if (c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
   service_pause(c);
   HIP_TRY(hipSetDevice(c->device));
@@ -419,6 +456,9 @@ void service_stop_wait(ricrc_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->svc_stream);
   c->svc_launched = false;
+  // whatever request is still unanswered is abandoned: a later wave starts
+  // after it (never answers it into a slot the host is refilling)
+  c->svc_served = (uint32_t)__atomic_load_n(&c->svc->req, __ATOMIC_ACQUIRE);
 }
 
 void service_atexit() {
@@ -429,6 +469,7 @@ void service_atexit() {
 
 int service_init(ricrc_ctx* c) {
   if (c->svc) return RICRC_OK;
+  HIP_TRY(device_busy_init(c->device, &c->busy));
   void* h = nullptr;
   HIP_TRY(hipHostMalloc(&h, ricrc::kSvcBytes, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(h, 0, sizeof(ricrc::ServiceRing));
@@ -460,7 +501,8 @@ void service_forget(ricrc_ctx* c) {
 // its idle timeout, or never ran.
 int service_ensure(ricrc_ctx* c) {
   const auto now = std::chrono::steady_clock::now();
-  if (c->svc_launched && __atomic_load_n(&c->svc->stop, __ATOMIC_ACQUIRE) == 0u) {
+  if (c->svc_launched && __atomic_load_n(&c->svc->stop, __ATOMIC_ACQUIRE) == 0u &&
+      __atomic_load_n(&c->svc->exited, __ATOMIC_ACQUIRE) == 0u) {
     // called again well within the idle timeout: the wave is still there
     // (no runtime query on the fast path); later, ask the stream
     if (now - c->svc_last < std::chrono::microseconds(c->svc_idle_us / 2) ||
@@ -477,8 +519,12 @@ int service_ensure(ricrc_ctx* c) {
   ricrc::ServiceArgs a{};
   a.ring = r;  // (unified addressing: the mapped host pointer is the device pointer)
   a.tables = c->d_tables;
-  a.served = (uint32_t)__atomic_load_n(&r->req, __ATOMIC_ACQUIRE);
+  // the last request ANSWERED, not the last published: a wave relaunched
+  // for a pending request (service_request) serves it first
+  a.served = c->svc_served;
   a.idle_ticks = (uint64_t)c->svc_idle_us * 100u;  // 100 MHz real-time counter
+  a.busy = c->busy;
+  a.busy_ticks = ricrc::kSvcBusyTicks;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   HIP_TRY(ricrc::launch_service(a, c->svc_stream));
   c->svc_launched = true;
@@ -506,22 +552,27 @@ int service_request(ricrc_ctx* c, uint32_t hi, uint64_t* answer, const uint64_t*
   };
   for (uint32_t spin = 1;; ++spin) {
     if (answered()) break;
-    if ((spin & 255u) == 0) {
-      // the wave may have left (idle timeout) just before the request was
-      // published: once its stream is idle and the answer is still missing,
-      // launch it again (it serves the pending request first)
-      if (hipStreamQuery(c->svc_stream) == hipSuccess && !answered()) {
+    if ((spin & 63u) == 0) {
+      // the wave may have left (idle timeout, a batch starting on the device,
+      // a stop) just before the request was published: once it has left and
+      // the answer is still missing, launch it again -- from the last
+      // ANSWERED sequence number, so it serves the pending request first
+      if (__atomic_load_n(&r->exited, __ATOMIC_ACQUIRE) != 0u && !answered()) {
         c->svc_launched = false;
         const int rc = service_ensure(c);
-        if (rc) return rc;
+        if (rc) {
+          c->svc_served = seq;  // (abandoned)
+          return rc;
+        }
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-        service_stop_wait(c);
+        service_stop_wait(c);  // (abandons it)
         return RICRC_EIO;
       }
     }
     __builtin_ia32_pause();
   }
+  c->svc_served = seq;
   if (answer) *answer = ans;
   return RICRC_OK;
 }

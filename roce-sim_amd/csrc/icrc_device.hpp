@@ -122,6 +122,19 @@ __device__ __forceinline__ void stg8(uint8_t* p, uint32_t v) {
 #endif
 constexpr int kPktStorePol = RICRC_PKT_STORE_POL;
 
+// Batch kernels announce themselves to the per-packet service waves resident
+// on the same device (icrc_service_kernel): thread 0 of every workgroup
+// stamps the 100 MHz real-time counter into the device's host-mapped busy
+// word as the workgroup starts (one 8-byte vector store over PCIe, posted).
+// A service wave that sees a young stamp leaves, so a workgroup of a batch
+// launched by ANY context that waits for the CU a wave holds (the wave's LDS
+// fills it) gets that CU within one poll of the wave's.
+__device__ __forceinline__ void announce_batch(uint64_t* busy) {
+  if (busy && threadIdx.x == 0)
+    __hip_atomic_store(busy, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }

@@ -29,6 +29,8 @@ struct IcrcArgs {
   // its range (epoch << 32 | next), nullable = static ranges only
   unsigned long long* claims;
   uint32_t epoch;
+  // the device's service busy word (host-mapped; nullable): see announce_batch
+  uint64_t* busy;
 };
 
 // Claim counters: per stream (up to kClaimStreams streams per context; later
@@ -81,6 +83,7 @@ struct SegArgs {
   const uint32_t* tables;
   unsigned long long* claims;  // tail-claim counters (nullable: static ranges only)
   uint32_t epoch;
+  uint64_t* busy;  // the device's service busy word (nullable): see announce_batch
 };
 
 // Enqueues the packet -> WR map kernel and the segmentation kernel.
@@ -140,7 +143,22 @@ struct ServiceArgs {
   const uint32_t* tables;
   uint32_t served;      // last request sequence number already answered
   uint64_t idle_ticks;  // 100 MHz ticks without a request before the wave leaves
+  // the device's busy word (host-mapped, 16 bytes): the real-time stamp of the
+  // latest batch workgroup start on this device; the wave leaves (when no
+  // request is pending) while the stamp is younger than busy_ticks
+  const uint64_t* busy;
+  uint64_t busy_ticks;
 };
+
+// Every service on a device shares one busy word; every batch kernel launched
+// on that device stamps it (announce_batch, icrc_device.hpp), so a batch
+// launched by ANY context gets the CUs that resident service waves hold
+// within one poll of theirs.  20 us of the 100 MHz counter: a batch's
+// workgroups start within a few microseconds of each other, and a wave
+// relaunched while a batch runs only finds a CU once one of the batch's
+// workgroups has finished, long after its stamp.
+constexpr uint64_t kSvcBusyTicks = 2000;
+constexpr size_t kBusyBytes = 128;  // one line per device
 
 // Enqueues the service kernel (one workgroup) on `stream`.
 hipError_t launch_service(const ServiceArgs& a, hipStream_t stream);

@@ -489,6 +489,7 @@ __global__ void __launch_bounds__(kStridedThreads, 1) icrc_strided_kernel(IcrcAr
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   const uint64_t c_start = __builtin_amdgcn_s_memtime();  // shader clock: the ratio is the GFX clock
 #endif
+  announce_batch(a.busy);
   stage_tables<LOG2G, kStridedThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 
@@ -628,6 +629,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 #ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+  announce_batch(a.busy);
   stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
 
   const int lane = tid & 63;
@@ -859,6 +861,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   constexpr int NB = LD::kBuckets;
   static_assert(W + 16 < 65536, "claims are 16-bit counters");
   const int tid = threadIdx.x;
+  announce_batch(a.busy);
   stage_tables<3, kIcrcThreads, MixedKeysL>(a.tables, tid);
   MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
 
@@ -1142,6 +1145,7 @@ template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out p
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
   const uint32_t S = (uint32_t)a.stride, L = a.len;
+  announce_batch(a.busy);
   const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
   const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
   const int ns = (n + 3) >> 2, pad = 4 * ns - n;  // steps, zero dwords in front
@@ -1575,7 +1579,10 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   uint32_t polls = 0;
   // one poll's value: 0 = nothing to do, 1 = a request served, 2 = leave
-  auto step = [&](const u32x4 head) -> int {
+  // the device's busy word (announce_batch): a batch workgroup started less
+  // than busy_ticks ago -> leave once no request is pending
+  const auto busy_rsrc = out_rsrc((void*)s.busy, s.busy ? 16u : 0u);  // (0 bytes: loads give 0)
+  auto step = [&](const u32x4 head, const u32x4 bz) -> int {
     const uint64_t req = (uint64_t)head.x | ((uint64_t)head.y << 32);
     const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)req);
     if (seq != served) {
@@ -1675,7 +1682,11 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
       return 1;
     }
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)head.z) != 0u) return 2;  // stop
-    if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) return 2;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    const uint64_t stamp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bz.x) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bz.y) << 32);
+    if (stamp != 0 && (int64_t)(now - stamp) < (int64_t)s.busy_ticks) return 2;  // a batch starts
+    if (now - t_last > s.idle_ticks) return 2;
     __builtin_amdgcn_s_sleep(2);
     return 0;
   };
@@ -1685,15 +1696,18 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   // flight: the next one is issued before this one's value is looked at, so
   // a request is seen about half a round trip sooner.  A poll issued before a
   // request was served shows its sequence number again (== served): ignored.
+  // The busy word is read beside the slot (both loads in flight together).
   auto poll = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, 0u, 0u, 17); };
-  u32x4 hA = poll();
+  auto poll_busy = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(busy_rsrc, 0u, 0u, 17); };
+  u32x4 hA = poll(), bA = poll_busy();
   for (;;) {
-    const u32x4 hB = poll();
+    const u32x4 hB = poll(), bB = poll_busy();
     ++polls;
-    if (step(hA) == 2) break;
+    if (step(hA, bA) == 2) break;
     hA = poll();
+    bA = poll_busy();
     ++polls;
-    if (step(hB) == 2) break;
+    if (step(hB, bB) == 2) break;
   }
   __builtin_amdgcn_s_waitcnt(0);  // the poll still in flight has returned
   if (lane == 0)  // the helper waves leave too

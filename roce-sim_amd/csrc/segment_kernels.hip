@@ -343,6 +343,7 @@ __global__ void __launch_bounds__(kSegThreads, 1) segment_kernel(SegArgs a) {
   constexpr int PPW = 64 / G;
   constexpr int U = kSegUnroll;
   const int tid = threadIdx.x;
+  announce_batch(a.busy);
   stage_tables<LOG2G, kSegThreads, MainKeys>(a.tables, tid);
   __syncthreads();
 

@@ -273,6 +273,11 @@ class RecvLoop:
             # verify: what it would receive is a RoCE datagram that passes the
             # ICRC; other datagrams a raw source sees, and frames dropped for
             # their ICRC, do not end the wait
+            # (packets an earlier batch verified and left queued are what the
+            # reference's socket would deliver at once)
+            bug = "BUG: just wait for timeout and it should not receive any packet"
+            if self._pending:
+                raise AssertionError(bug)
             deadline = None if self.timeout is None else time.monotonic() + self.timeout
             while True:
                 left = None if deadline is None else deadline - time.monotonic()
@@ -283,8 +288,7 @@ class RecvLoop:
                 except socket.timeout:
                     return []
                 if self._pending:
-                    raise AssertionError(
-                        "BUG: just wait for timeout and it should not receive any packet")
+                    raise AssertionError(bug)
         out = []
         while len(out) < npkt:
             if not self._pending:

@@ -196,3 +196,25 @@ def test_bench_two_rank_cfg4_rehearsal(tmp_path):
     assert line["parity"]["mismatches_per_rank"] == [0, 0]
     assert line["parity"]["sampled_per_rank"] == [40000, 40000]
     assert line["checks"]["pass"]
+
+
+def test_plain_bench_gpus2_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher (the driver's form): bench.py
+    starts the two ranks itself, so the line is a 2-rank cfg4 line with a
+    CPU baseline over rank 0's shard (one device when only one is visible)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    if _ndev() < 2:
+        env["ROCE_ICRC_BENCH_DEVICE"] = "0"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
+           "--packets", "40000"]
+    r = subprocess.run(cmd, env=env, cwd=str(ROOT), capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only, once
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["workload"].startswith("cfg4")
+    assert line["parity"]["mismatches_per_rank"] == [0, 0]
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["parity_mismatches_vs_gpu"] == 0
+    assert cpu["sample"].startswith("rank 0's shard (40000 packets of 80000)")

@@ -68,6 +68,17 @@ def test_npkt_zero_expects_the_timeout():
     assert loop.stats.not_roce == 2 and loop.stats.icrc_dropped == 1
 
 
+def test_npkt_zero_sees_packets_an_earlier_batch_left_queued():
+    """A batch larger than npkt leaves verified packets queued: the reference's
+    socket would deliver the next one at once, so recv_pkts(0) asserts without
+    waiting on the source (which here would only time out)."""
+    fr = _frames(4)
+    loop = RV.RecvLoop(RV.ListSource(fr), batch=4, verify=oracle_verify)
+    assert loop.recv_pkts(1) == [0x01]  # one batch of 4 verified, 3 left queued
+    with pytest.raises(AssertionError, match="should not receive"):
+        loop.recv_pkts(0)
+
+
 def _raw_pair():
     try:
         return RV.RawIpSink(), RV.RawSocketSource()
