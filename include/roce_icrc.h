@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define RICRC_ABI_VERSION 3
+#define RICRC_ABI_VERSION 4
 
 /* call-level return codes */
 #define RICRC_OK 0
@@ -141,11 +141,24 @@ int ricrc_compute_strided(ricrc_ctx* ctx, const uint8_t* frames, uint64_t stride
                           uint32_t n, uint32_t* icrc_out, uint8_t* status_out /* nullable */);
 
 /* Round-robin split over several contexts (one per GPU): packet i goes to
- * ctxs[i % nctx]; host threads gather, copy, launch and scatter per device. */
+ * ctxs[i % nctx] (per-packet independence, src/roce.py:192-219).  One host
+ * thread per distinct context streams its shard in chunks through two pinned
+ * staging blocks the context owns (gather of chunk k + 1 overlaps the copies
+ * and kernel of chunk k); contexts named more than once run their shards one
+ * after another. */
 int ricrc_compute_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
                               size_t frames_bytes, const uint64_t* offsets,
                               const uint32_t* lens, uint32_t n, uint32_t* icrc_out,
                               uint8_t* status_out /* nullable */);
+/* The receive side of the same split: what RoCEv2.recv_pkts
+ * (src/roce_v2.py:327-372) would call with one received batch on a node of
+ * several GPUs.  ok_out[i] = 1 iff frame i's trailer equals its ICRC (the
+ * ricrc_verify_batch rule). */
+int ricrc_verify_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
+                             size_t frames_bytes, const uint64_t* offsets,
+                             const uint32_t* lens, uint32_t n, uint8_t* ok_out,
+                             uint32_t* icrc_out /* nullable */,
+                             uint8_t* status_out /* nullable */);
 
 /* Page-lock a caller buffer so the H2D/D2H copies above run at DMA speed. */
 int ricrc_host_register(void* ptr, size_t bytes);

@@ -66,6 +66,16 @@ struct ricrc_ctx {
   uint64_t* busy = nullptr;  // the device's service busy word (device_busy), once any service ran
   uint32_t svc_idle_us = 1000;  // 0 = service off (staged launch per call)
   std::chrono::steady_clock::time_point svc_last{};  // last call (the wave's idle clock)
+  // multi-device host entry points (ricrc_*_batch_multi): two pinned staging
+  // blocks with device twins, so the gather of one chunk overlaps the
+  // previous chunk's copies and kernel (see multi_shard)
+  struct Stage {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    hipEvent_t ev = nullptr;
+  };
+  Stage ms[2];
+  size_t ms_frames = 0;  // frame bytes each block holds
 };
 
 namespace {
@@ -697,6 +707,175 @@ int thread_ctx(int device, ricrc_ctx** out) {
   return RICRC_OK;
 }
 
+// ---- multi-device host split (ricrc_compute/verify_batch_multi) ------------
+// Packet i of the caller's batch belongs to shard i mod nctx.  Each shard is
+// streamed through its context in chunks: the host gathers a chunk's frames
+// (dword-aligned), offsets and lengths into a pinned block, then one H2D copy
+// of the frames, one of the descriptors, the ragged kernel, and one D2H copy
+// of [icrc | status | ok] go onto the context's stream.  Two blocks alternate,
+// so while the GPU side of chunk k runs the host gathers chunk k + 1 and
+// scatters chunk k - 1.  (Round 3 gathered a whole shard into a pageable
+// std::vector per call and copied from it: no overlap, and the copies ran
+// through the runtime's pageable staging.)
+constexpr size_t kMultiChunkFrames = 8u << 20;
+constexpr uint32_t kMultiChunkPkts = 1u << 16;
+size_t multi_desc_off(size_t frames) { return up256(frames); }
+size_t multi_out_off(size_t frames) {
+  return multi_desc_off(frames) + up256(12ull * kMultiChunkPkts);
+}
+size_t multi_block(size_t frames) { return multi_out_off(frames) + 6ull * kMultiChunkPkts; }
+
+void multi_free(ricrc_ctx* c) {
+  for (auto& s : c->ms) {
+    if (s.ev) (void)hipEventDestroy(s.ev);
+    if (s.h) (void)hipHostFree(s.h);
+    (void)hipFree(s.d);
+    s = ricrc_ctx::Stage{};
+  }
+  c->ms_frames = 0;
+}
+
+int multi_ensure(ricrc_ctx* c, size_t frames) {
+  frames = frames < kMultiChunkFrames ? kMultiChunkFrames : up256(frames);
+  if (frames <= c->ms_frames) return RICRC_OK;
+  multi_free(c);
+  for (auto& s : c->ms) {
+    hipError_t e = hipHostMalloc((void**)&s.h, multi_block(frames), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&s.d, multi_block(frames));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      multi_free(c);
+      return hip_fail(e);
+    }
+  }
+  c->ms_frames = frames;
+  return RICRC_OK;
+}
+
+struct MultiBatch {
+  const uint8_t* frames;
+  const uint64_t* offsets;
+  const uint32_t* lens;
+  uint64_t n;
+  uint32_t stride;  // nctx: shard d holds packets d, d + stride, ...
+  uint32_t* icrc_out;
+  uint8_t* status_out;
+  uint8_t* ok_out;
+  bool verify;
+};
+
+int multi_shard(ricrc_ctx* c, const MultiBatch& b, uint32_t d) {
+  if (d >= b.n) return RICRC_OK;
+  uint32_t maxlen = 0;
+  for (uint64_t i = d; i < b.n; i += b.stride) maxlen = b.lens[i] > maxlen ? b.lens[i] : maxlen;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = multi_ensure(c, ((size_t)maxlen + 3u) & ~(size_t)3u);
+  if (rc) return rc;
+  const size_t cap = c->ms_frames, o_desc = multi_desc_off(cap), o_out = multi_out_off(cap);
+  struct Pending {
+    uint64_t first = 0;  // shard index of the chunk's first packet
+    uint32_t m = 0;
+  } pend[2];
+  // copy a finished chunk's answers to the caller's arrays
+  auto scatter = [&](int s) {
+    Pending& p = pend[s];
+    if (!p.m) return RICRC_OK;
+    HIP_TRY(hipEventSynchronize(c->ms[s].ev));
+    const uint8_t* h = c->ms[s].h + o_out;
+    const uint32_t* ic = (const uint32_t*)h;
+    const uint8_t* st = h + 4ull * p.m;
+    const uint8_t* ok = st + p.m;
+    uint64_t i = d + p.first * b.stride;
+    for (uint32_t k = 0; k < p.m; ++k, i += b.stride) {
+      if (b.icrc_out) b.icrc_out[i] = ic[k];
+      if (b.status_out) b.status_out[i] = st[k];
+      if (b.verify) b.ok_out[i] = ok[k];
+    }
+    p.m = 0;
+    return RICRC_OK;
+  };
+  const uint64_t total = (b.n - d + b.stride - 1) / b.stride;  // packets in this shard
+  uint64_t next = 0;
+  int s = 0;
+  while (next < total) {
+    rc = scatter(s);  // the block's previous chunk (two chunks ago) is done
+    if (rc) return rc;
+    uint8_t* h = c->ms[s].h;
+    uint64_t* offs = (uint64_t*)(h + o_desc);
+    uint32_t m = 0;
+    size_t pos = 0;
+    const uint64_t first = next;
+    for (uint64_t i = d + next * b.stride; next < total && m < kMultiChunkPkts; i += b.stride) {
+      const uint32_t L = b.lens[i];
+      const size_t slot = ((size_t)L + 3u) & ~(size_t)3u;
+      if (pos + slot > cap) break;
+      std::memcpy(h + pos, b.frames + b.offsets[i], L);
+      offs[m++] = pos;
+      pos += slot;
+      ++next;
+    }
+    // lengths right after the chunk's m offsets: one descriptor copy
+    uint32_t* ls = (uint32_t*)(offs + m);
+    for (uint32_t k = 0; k < m; ++k) ls[k] = b.lens[d + (first + k) * b.stride];
+    uint8_t* dv = c->ms[s].d;
+    if (pos) HIP_TRY(hipMemcpyAsync(dv, h, pos, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dv + o_desc, h + o_desc, 12ull * m, hipMemcpyHostToDevice, c->stream));
+    uint32_t* d_icrc = (uint32_t*)(dv + o_out);
+    uint8_t* d_st = dv + o_out + 4ull * m;
+    rc = launch(c, dv, (const uint64_t*)(dv + o_desc), (const uint32_t*)(dv + o_desc + 8ull * m), 0,
+                0, m, d_icrc, d_st, b.verify ? d_st + m : nullptr, true, b.verify,
+                ragged_log2g(c, (uint32_t)(pos / m)), c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(h + o_out, dv + o_out, (b.verify ? 6ull : 5ull) * m,
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->ms[s].ev, c->stream));
+    pend[s] = {first, m};
+    s ^= 1;
+  }
+  rc = scatter(s);
+  if (rc) return rc;
+  return scatter(s ^ 1);
+}
+
+int batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames, size_t frames_bytes,
+                const uint64_t* offsets, const uint32_t* lens, uint32_t n, uint32_t* icrc_out,
+                uint8_t* status_out, uint8_t* ok_out, bool verify) {
+  if (!ctxs || nctx < 1 || (verify ? !ok_out : !icrc_out) || (n && (!frames || !offsets || !lens)))
+    return RICRC_EINVAL;
+  for (int d = 0; d < nctx; ++d)
+    if (!ctxs[d]) return RICRC_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
+  const MultiBatch b{frames, offsets, lens, n, (uint32_t)nctx, icrc_out, status_out, ok_out, verify};
+  // A context is single-threaded: shards that name the same context run one
+  // after another on that context's thread.
+  std::vector<ricrc_ctx*> uniq;
+  std::vector<std::vector<int>> shards_of;
+  for (int d = 0; d < nctx; ++d) {
+    size_t u = 0;
+    while (u < uniq.size() && uniq[u] != ctxs[d]) ++u;
+    if (u == uniq.size()) {
+      uniq.push_back(ctxs[d]);
+      shards_of.emplace_back();
+    }
+    shards_of[u].push_back(d);
+  }
+  std::vector<int> rcs(nctx, RICRC_OK);
+  auto run = [&](size_t u) {
+    for (int d : shards_of[u]) {
+      rcs[d] = multi_shard(uniq[u], b, (uint32_t)d);
+      if (rcs[d]) return;
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t u = 1; u < uniq.size(); ++u) th.emplace_back(run, u);
+  run(0);  // (the calling thread takes the first context)
+  for (auto& t : th) t.join();
+  for (int d = 0; d < nctx; ++d)
+    if (rcs[d]) return rcs[d];
+  return RICRC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -775,6 +954,7 @@ void ricrc_ctx_destroy(ricrc_ctx* c) {
   (void)hipFree(c->d_mr);
   (void)hipFree(c->d_wrs);
   (void)hipFree(c->d_stage);
+  multi_free(c);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->svc) (void)hipHostFree(c->svc);
   if (c->svc_stream) (void)hipStreamDestroy(c->svc_stream);
@@ -878,65 +1058,16 @@ int ricrc_compute_strided(ricrc_ctx* c, const uint8_t* frames, uint64_t stride, 
 int ricrc_compute_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
                               size_t frames_bytes, const uint64_t* offsets, const uint32_t* lens,
                               uint32_t n, uint32_t* icrc_out, uint8_t* status_out) {
-  if (!ctxs || nctx < 1 || !icrc_out || (n && (!frames || !offsets || !lens))) return RICRC_EINVAL;
-  for (int d = 0; d < nctx; ++d)
-    if (!ctxs[d]) return RICRC_EINVAL;
-  for (uint32_t i = 0; i < n; ++i)
-    if (offsets[i] > frames_bytes || lens[i] > frames_bytes - offsets[i]) return RICRC_EINVAL;
-  // A context is single-threaded: shards that name the same context run one
-  // after another on that context's thread.
-  std::vector<ricrc_ctx*> uniq;
-  std::vector<std::vector<int>> shards_of;
-  for (int d = 0; d < nctx; ++d) {
-    size_t u = 0;
-    while (u < uniq.size() && uniq[u] != ctxs[d]) ++u;
-    if (u == uniq.size()) {
-      uniq.push_back(ctxs[d]);
-      shards_of.emplace_back();
-    }
-    shards_of[u].push_back(d);
-  }
-  std::vector<int> rcs(nctx, RICRC_OK);
-  auto run_shard = [&](int d) {
-    // gather packets d, d + nctx, ... into one contiguous host slice
-    std::vector<uint64_t> offs;
-    std::vector<uint32_t> ls;
-    size_t bytes = 0;
-    for (uint64_t i = d; i < n; i += nctx) {
-      offs.push_back(bytes);
-      ls.push_back(lens[i]);
-      bytes += ((uint64_t)lens[i] + 3u) & ~(uint64_t)3u;  // keep every frame dword aligned
-    }
-    const uint32_t m = (uint32_t)offs.size();
-    if (m == 0) return;
-    std::vector<uint8_t> buf;
-    std::vector<uint32_t> out(m);
-    std::vector<uint8_t> st(m);
-    try {
-      buf.resize(bytes);
-    } catch (...) {
-      rcs[d] = RICRC_ENOMEM;
-      return;
-    }
-    for (uint32_t k = 0; k < m; ++k)
-      std::memcpy(buf.data() + offs[k], frames + offsets[(uint64_t)k * nctx + d], ls[k]);
-    rcs[d] = ricrc_compute_batch(ctxs[d], buf.data(), bytes, offs.data(), ls.data(), m,
-                                 out.data(), st.data());
-    if (rcs[d]) return;
-    for (uint32_t k = 0; k < m; ++k) {
-      icrc_out[(uint64_t)k * nctx + d] = out[k];
-      if (status_out) status_out[(uint64_t)k * nctx + d] = st[k];
-    }
-  };
-  std::vector<std::thread> th;
-  for (size_t u = 0; u < uniq.size(); ++u)
-    th.emplace_back([&, u] {
-      for (int d : shards_of[u]) run_shard(d);
-    });
-  for (auto& t : th) t.join();
-  for (int d = 0; d < nctx; ++d)
-    if (rcs[d]) return rcs[d];
-  return RICRC_OK;
+  return batch_multi(ctxs, nctx, frames, frames_bytes, offsets, lens, n, icrc_out, status_out,
+                     nullptr, false);
+}
+
+int ricrc_verify_batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames,
+                             size_t frames_bytes, const uint64_t* offsets, const uint32_t* lens,
+                             uint32_t n, uint8_t* ok_out, uint32_t* icrc_out,
+                             uint8_t* status_out) {
+  return batch_multi(ctxs, nctx, frames, frames_bytes, offsets, lens, n, icrc_out, status_out,
+                     ok_out, true);
 }
 
 int ricrc_host_register(void* ptr, size_t bytes) {

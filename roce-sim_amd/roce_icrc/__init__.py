@@ -16,6 +16,7 @@ from .engine import (  # noqa: F401
     IcrcError,
     IcrcUnavailable,
     compute_batch_multi,
+    verify_batch_multi,
     load_library,
     pack_aligned,
     pack_icrc,

@@ -100,6 +100,10 @@ _SIGNATURES = {
         ctypes.c_int,
         [_vp, ctypes.c_int, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_uint32, _vp, _vp],
     ),
+    "ricrc_verify_batch_multi": (
+        ctypes.c_int,
+        [_vp, ctypes.c_int, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp],
+    ),
     "ricrc_host_register": (ctypes.c_int, [_vp, ctypes.c_size_t]),
     "ricrc_host_unregister": (ctypes.c_int, [_vp]),
     "ricrc_compute_batch_dev": (
@@ -477,6 +481,25 @@ def compute_batch_multi(engines: list[IcrcEngine], frames, offsets, lens):
     if rc != RICRC_OK:
         raise IcrcError("ricrc_compute_batch_multi", rc, lib.ricrc_strerror(rc).decode())
     return out, st
+
+
+def verify_batch_multi(engines: list[IcrcEngine], frames, offsets, lens):
+    """Receive-side round-robin split (packet i -> engines[i % len]): what
+    RoCEv2.recv_pkts (src/roce_v2.py:327-372) would call with one received
+    batch on a node of several GPUs.  Returns (ok, icrc, status)."""
+    lib = load_library()
+    f = _u8(frames)
+    offs, ls = _descriptors(offsets, lens)
+    n = offs.size
+    arr = (_vp * len(engines))(*[e.ctx.value for e in engines])
+    ok = np.zeros(n, np.uint8)
+    out = np.zeros(n, np.uint32)
+    st = np.zeros(n, np.uint8)
+    rc = lib.ricrc_verify_batch_multi(arr, len(engines), _ptr(f), f.size, _ptr(offs), _ptr(ls),
+                                      n, _ptr(ok), _ptr(out), _ptr(st))
+    if rc != RICRC_OK:
+        raise IcrcError("ricrc_verify_batch_multi", rc, lib.ricrc_strerror(rc).decode())
+    return ok.astype(bool), out, st
 
 
 def pack_icrc(icrc: int) -> bytes:

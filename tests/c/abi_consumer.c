@@ -45,6 +45,16 @@ static int gpu_leg(ricrc_ctx* ctx, int ndev) {
   if (ricrc_verify_batch(ctx, buf, sizeof buf, offs, lens, 3, ok, NULL, NULL) != RICRC_OK)
     return 24;
   if (ok[0] != 1 || ok[1] != 0 || ok[2] != 1) return 25;
+  {  /* the receive-side split, one context named twice (any box) */
+    ricrc_ctx* same[2] = {ctx, ctx};
+    uint8_t okm[3] = {9, 9, 9};
+    uint32_t mm[3] = {0, 0, 0};
+    if (ricrc_verify_batch_multi(same, 2, buf, sizeof buf, offs, lens, 3, okm, mm, NULL) !=
+        RICRC_OK)
+      return 29;
+    if (okm[0] != 1 || okm[1] != 0 || okm[2] != 1 || mm[0] != out[0] || mm[1] != out[1])
+      return 30;
+  }
   if (ndev >= 2) {
     ricrc_ctx* c2 = NULL;
     if (ricrc_ctx_create(1, &c2) != RICRC_OK) return 26;

@@ -86,6 +86,17 @@ def test_compute_batch_multi_on_distinct_devices():
         # a context list naming one device twice, the others once
         got2, _ = E.compute_batch_multi(engines + engines[:1], buf, offs, lens)
         np.testing.assert_array_equal(got2, want)
+        # the receive-side split (ricrc_verify_batch_multi) over the stamped
+        # stream, one trailer broken per device
+        for i in range(n_total):
+            e = int(offs[i]) + int(lens[i])
+            buf[e - 4:e] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+        bad = np.arange(nd) + 1000
+        for i in bad:
+            buf[int(offs[i]) + 100] ^= 1
+        ok, icrc, _ = E.verify_batch_multi(engines, buf, offs, lens)
+        assert ok.sum() == n_total - nd and not ok[bad].any()
+        np.testing.assert_array_equal(np.delete(icrc, bad), np.delete(want, bad))
     finally:
         for e in engines:
             e.close()

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 import icrc_oracle as o  # noqa: E402  (checker only)
 from roce_icrc import synth  # noqa: E402
 from roce_icrc.engine import (  # noqa: E402
-    PKT_BAD_LEN, PKT_ICRC_MISMATCH, PKT_LEN_MISMATCH, PKT_NOT_IPV4, PKT_NOT_UDP)
+    PKT_BAD_LEN, PKT_FATAL, PKT_ICRC_MISMATCH, PKT_LEN_MISMATCH, PKT_NOT_IPV4, PKT_NOT_UDP)
 
 LANES = [1, 2, 4, 8, 16, 32, 64]
 
@@ -456,6 +456,54 @@ def test_multi_context_round_robin(engine):
         e2.close()
     want, _ = oracle_batch(buf, offs, lens)
     np.testing.assert_array_equal(got, want)
+
+
+def test_multi_chunked_compute_and_verify(engine):
+    """The multi split streams each shard in chunks (8 MiB of frames or 65536
+    packets) through two pinned blocks: shards of many chunks, a chunk boundary
+    inside a run of ACK-sized frames, odd lengths, and one 9 MiB non-frame
+    (status BAD_LEN, ICRC 0) that forces the blocks to grow.  compute and
+    verify through the C ABI against the oracle; verify flags exactly the
+    corrupted frames (src/roce_v2.py:327-372 is the receive batch it serves)."""
+    from roce_icrc import IcrcEngine, compute_batch_multi, verify_batch_multi
+    big_buf, big_offs, big_lens = synth.mixed_mtu_frames(30000, seed=21)
+    tiny_buf, tiny_offs, tiny_lens = synth.mixed_mtu_frames(300000, seed=22, mtus=(0,))
+    huge = np.random.default_rng(3).integers(0, 256, 9 << 20, dtype=np.uint8)
+    parts = [(big_buf, big_offs, big_lens), (tiny_buf, tiny_offs, tiny_lens),
+             (huge, np.zeros(1, np.uint64), np.array([huge.size], np.uint32))]
+    buf = np.concatenate([p[0] for p in parts])
+    base = np.cumsum([0] + [p[0].size for p in parts[:-1]]).astype(np.uint64)
+    offs = np.concatenate([p[1] + b for p, b in zip(parts, base)])
+    lens = np.concatenate([p[2] for p in parts]).astype(np.uint32)
+    lens[7] -= 2  # odd length (CRC'd as zlib would; IP length mismatch status)
+    rng = np.random.default_rng(5)
+    perm = rng.permutation(offs.size)  # interleave the families across shards
+    offs, lens = offs[perm], lens[perm]
+    want, _ = oracle_batch(buf, offs, lens)
+    good = lens <= 65535  # (the 9 MiB one: the reference's "warning + ICRC 0" path)
+    assert (~good).sum() == 1 and want[~good][0] == 0
+    e2 = IcrcEngine(0)
+    try:
+        got, st = compute_batch_multi([engine, e2, e2], buf, offs, lens)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal((st & PKT_FATAL) != 0, ~good)
+        assert st[np.flatnonzero(perm == 7)[0]] == PKT_LEN_MISMATCH
+        # stamp the answers, corrupt 97 frames, verify on the same split
+        for i in range(offs.size):
+            e = int(offs[i]) + int(lens[i])
+            if lens[i] <= 65535 and lens[i] >= 4:
+                buf[e - 4:e] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+        bad = rng.choice(np.flatnonzero(good), 97, replace=False)
+        for i in bad:
+            buf[int(offs[i]) + int(lens[i]) - 1] ^= 0x40  # the ICRC trailer's top byte
+        ok, icrc, st2 = verify_batch_multi([e2, engine], buf, offs, lens)
+        want_ok = good.copy()
+        want_ok[bad] = False
+        np.testing.assert_array_equal(ok, want_ok)
+        np.testing.assert_array_equal(icrc, want)
+        assert ((st2 & PKT_ICRC_MISMATCH) != 0).sum() == 97
+    finally:
+        e2.close()
 
 
 def test_full_size_cfg2_bit_exact(engine):
