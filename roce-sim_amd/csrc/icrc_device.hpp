@@ -344,21 +344,11 @@ using Keys8 = Keys8T<0>;
 // 12-wave build (2 A/B rounds): cfg2 equal with all three, cfg3 Keys8 -1.1 %
 // and Keys16 -1.8 % even with one sort window per workgroup.  The small
 // kernel uses Keys8.
-#ifdef RICRC_TABLES16
-using MainKeys = Keys16;
-#elif defined(RICRC_TABLES8)
-using MainKeys = Keys8;
-#else
 using MainKeys = Keys32;
-#endif
 
 template <class K>
 __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w, const K& k) {
-#ifdef RICRC_ABLATE_FOLD  // diagnostic build only: loads kept, table folding removed
-  P ^= w;
-#else
   k.absorb(P, T, w);
-#endif
 }
 
 template <class K>

@@ -136,14 +136,10 @@ __device__ __forceinline__ u32x4 load_chunk(const Pkt& p, int j, int gl) {
   const int kb = DPI * j + 4 * gl - p.S;
   u32x4 v = {0, 0, 0, 0};
   if (!p.dead && kb + 3 >= 0 && kb < p.n) {
-#ifdef RICRC_EDGE_NT  // diagnostic build only: edge chunks non-temporal like the body
-    v = ldg128(p.ab + 16 * (G * j + gl));
-#else
     if constexpr (SHARED)
       v = *(const u32x4*)(p.ab + 16 * (G * j + gl));
     else
       v = ldg128(p.ab + 16 * (G * j + gl));
-#endif
   }
   return v;
 }
@@ -285,11 +281,7 @@ __device__ __forceinline__ Batch<kUnroll> issue_packet(const Pkt& p, int gl) {
     const uint8_t* q = body_addr<G>(p, jhh, gl);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-#ifdef RICRC_FIRST_BLOCK_PLAIN  // experiment: the first body block cached as well
-      b.cur[u] = u < first ? *(const u32x4*)(q + 16 * G * u) : u32x4{0, 0, 0, 0};
-#else
       b.cur[u] = u < first ? ldg128(q + 16 * G * u) : u32x4{0, 0, 0, 0};
-#endif
   }
   b.wl = load_chunk<G>(p, JL, gl);
   return b;
@@ -429,11 +421,7 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
     B = slow_packet<LOG2G, K>(p.unal ? describe<DPI>(p.fp, p.pkt, true, 0, p.L, true) : p, ihl, gl,
                               base);
   const uint32_t icrc = good ? ~B : 0u;
-#ifdef RICRC_ABLATE_OUT  // diagnostic build only: per-packet output stores removed (kept live)
-  if (p.live && gl == 0 && icrc == 0x9E3779B9u) {
-#else
   if (p.live && gl == 0) {
-#endif
     if constexpr (VERIFY) {
       const bool ok = good && trailer == icrc;
       if (good && !ok) st |= kPktIcrcMismatch;
@@ -450,9 +438,7 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
       else
         stg32<kPktStorePol>(a.icrc_out + p.pkt, icrc);
     }
-#ifndef RICRC_BLOCK_TIMES
     if (a.status_out) stg8<kPktStorePol>(a.status_out + p.pkt, st);
-#endif
   }
 }
 
@@ -485,10 +471,6 @@ __global__ void __launch_bounds__(kStridedThreads, 1) icrc_strided_kernel(IcrcAr
   constexpr int G = 1 << LOG2G;
   constexpr int PPW = 64 / G;  // packets per wave step
   const int tid = threadIdx.x;
-#ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  const uint64_t c_start = __builtin_amdgcn_s_memtime();  // shader clock: the ratio is the GFX clock
-#endif
   announce_batch(a.busy);
   stage_tables<LOG2G, kStridedThreads, MainKeys>(a.tables, tid);
   __syncthreads();
@@ -582,15 +564,6 @@ __global__ void __launch_bounds__(kStridedThreads, 1) icrc_strided_kernel(IcrcAr
     for (uint32_t i = (ob.cap & ~3u) + (uint32_t)tid; i < ob.cap; i += kStridedThreads)
       out_store32<kStridedOutPol>(lds_rd(kOutLds<LOG2G> + 4u * i), dst, 4u * i);
   }
-#ifdef RICRC_BLOCK_TIMES
-  __syncthreads();
-  if (tid == 0 && a.status_out) {
-    ((uint64_t*)a.status_out)[2 * blockIdx.x] = t_start;
-    ((uint64_t*)a.status_out)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-    ((uint64_t*)a.status_out)[2 * gridDim.x + 2 * blockIdx.x] = c_start;
-    ((uint64_t*)a.status_out)[2 * gridDim.x + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime();
-  }
-#endif
 }
 
 // Ragged frames (offsets[i], lens[i]).  The lanes of a wave fold their
@@ -626,9 +599,6 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
   constexpr int NB = LD::kBuckets;
   static_assert(W + kIcrcWaves < 65536, "set claims are 16-bit counters");
   const int tid = threadIdx.x;
-#ifdef RICRC_BLOCK_TIMES  // diagnostic build only: per-block start/end clocks into status_out
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
   announce_batch(a.busy);
   stage_tables<LOG2G, kIcrcThreads, MainKeys>(a.tables, tid);
 
@@ -739,9 +709,6 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
       ob.ok_cap = (uint32_t)cnt;
       ob.ok_lds = LD::kOk;
     }
-#ifdef RICRC_RAGGED_SORT_ONLY  // diagnostic build only: windows sorted, no set processed
-    if (nsets < 0)
-#endif
     for (;;) {
       uint32_t old = 0;
       if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? 0x10000u : 1u);
@@ -758,12 +725,6 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
       for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
     }
   }
-#ifdef RICRC_BLOCK_TIMES
-  if (tid == 0 && a.status_out) {
-    ((uint64_t*)a.status_out)[2 * blockIdx.x] = t_start;
-    ((uint64_t*)a.status_out)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -992,9 +953,6 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
                     : (uint32_t)__builtin_amdgcn_readfirstlane(
                           (int)rlen[from_back ? cnt - 1 : ntiny + min(15, nb - 1)]) <= kMixedShortLen
                         ? 16u : 8u;
-#ifdef RICRC_RAGGED_SORT_ONLY  // diagnostic build only: windows sorted, no set processed
-    if (cnt < 0)
-#endif
     for (;;) {
       uint32_t old = 0;
       if (lane == 0) old = atomicAdd((uint32_t*)claim, from_back ? (size << 16) : size);
@@ -1205,16 +1163,12 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
         if (good && !ok) st |= kPktIcrcMismatch;
         a.ok_out[pkt] = ok ? 1 : 0;
       }
-#ifdef RICRC_SMALL_STORE_RING  // diagnostic build only: outputs wrap in a ring of that many dwords
-      if constexpr ((OUTS & 1) != 0) a.icrc_out[pkt & (RICRC_SMALL_STORE_RING - 1u)] = icrc;
-#else
       if constexpr ((OUTS & 1) != 0) {
         if (kRing && to_ring)
           lds_wr(small_ring_word(ring, pkt - ring_base), icrc);
         else
           a.icrc_out[pkt] = icrc;
       }
-#endif
       if constexpr ((OUTS & 2) != 0) a.status_out[pkt] = (uint8_t)st;
     }
   };
@@ -1268,19 +1222,6 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   };
   auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext, bool live = true,
                             bool to_ring = true) {  // (to the ring when there is one)
-#ifdef RICRC_SMALL_ABLATE_STAGE  // diagnostic build only: loads and output stores, no LDS, no fold
-    {
-      u32x4 acc = Rg[0];
-#pragma unroll
-      for (int t = 1; t < C; ++t) acc ^= Rg[t];
-      load(bnext, Rg);
-#ifdef RICRC_SMALL_ABLATE_STORE  // ... and no output stores
-      if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u)
-#endif
-        emit(b * 64u + (uint32_t)lane, true, 0u, acc.x ^ acc.y ^ acc.z ^ acc.w, 0u);
-      return;
-    }
-#endif
     // staging and the prefetch go out at raised wave priority: cfg5 +2.5 to
     // +12 % (4326 -> 4437-4855 GiB/s, 6 A/B rounds on two boxes; priority 1-2
     // +2-3 %; raising it for the output stores as well measured 12 % slower,
@@ -1305,11 +1246,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
       __asm__ __volatile__("" ::: "memory");
       const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
-#ifdef RICRC_SMALL_ABLATE_FOLD  // diagnostic build only: staging kept, fold removed
-      R = lds_rd(pz + 16u) ^ lds_rd(pz + 60u);
-#else
       R = fold4([&](int, int kp) { return lds_rd(pz + 4u * (uint32_t)kp); });
-#endif
     } else {
       R = small_fold_masked<false>(nullptr, pb, ihl, n);
     }
