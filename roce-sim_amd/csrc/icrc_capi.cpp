@@ -587,7 +587,10 @@ int service_request(ricrc_ctx* c, uint32_t hi, uint64_t* answer, const uint64_t*
   return RICRC_OK;
 }
 
-// One frame through the resident wave.
+// One frame through the resident wave.  A frame of at most 48 bytes (ACK,
+// NAK, read request, atomic ack) also rides in the slot's first 64 bytes,
+// which the wave's poll reads with the request word: no second PCIe read for
+// its bytes (ServiceRing::inline_frame).
 int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icrc_out,
                  uint8_t* status_out) {
   int rc = service_init(c);
@@ -595,8 +598,18 @@ int service_call(ricrc_ctx* c, const uint8_t* frame, uint32_t len, uint32_t* icr
   rc = service_ensure(c);
   if (rc) return rc;
   std::memcpy((uint8_t*)c->svc + ricrc::kSvcFrame, frame, len);
+  uint32_t hi = len;
+  if (len <= ricrc::kSvcInlineMax) {
+    const uint32_t next = c->svc_seq + 1 == 0 ? 1u : c->svc_seq + 1;  // (service_request's seq)
+    uint32_t d12[12] = {0};
+    std::memcpy(d12, frame, len);
+    std::memcpy(c->svc->inline_frame, d12, sizeof d12);
+    // (ordered before the request word by service_request's release store)
+    __atomic_store_n(&c->svc->check, ricrc::svc_inline_check(next, d12), __ATOMIC_RELAXED);
+    hi |= ricrc::kSvcInline;
+  }
   uint64_t ans = 0;
-  rc = service_request(c, len, &ans);
+  rc = service_request(c, hi, &ans);
   if (rc) return rc;
   *icrc_out = (uint32_t)ans;
   if (status_out) *status_out = (uint8_t)(ans >> 32);

@@ -107,7 +107,15 @@ struct ServiceRing {
   // once (a separate length word cost a second round trip, ~1.5 us)
   uint64_t req;
   uint32_t stop;  // host: 1 = leave now
-  uint32_t pad0[29];
+  // host: an inline request (kSvcInline, round 4) carries its frame (<= 48 B)
+  // in the rest of the slot's first 64 bytes, which the wave's poll reads
+  // anyway (one 64-byte load: the request needs no second PCIe round trip for
+  // its bytes); `check` = svc_inline_check(seq, the 48 bytes), written with
+  // the frame before req, so a poll that saw req but not all of the frame's
+  // bytes (a torn read) is recognised and served from kSvcFrame instead
+  uint32_t check;
+  uint8_t inline_frame[48];
+  uint32_t pad0[16];
   // GPU: the answer, ONE 8-byte store: ICRC (bits 0-31), status (32-39) and
   // the request's sequence number mod 2^24 (40-63) -- no fence between a
   // result and its sequence number
@@ -131,12 +139,22 @@ constexpr uint32_t kSvcMaxFrame = 65536;
 constexpr uint32_t kSvcMaxBurst = 64;
 __host__ __device__ inline uint32_t svc_burst_tag(uint32_t seq) { return (seq & 0x7FFFu) | 0x8000u; }
 constexpr uint32_t kSvcBurst = 0x80000000u, kSvcVerify = 0x40000000u;
+constexpr uint32_t kSvcInline = 0x20000000u;  // single frame, also in ServiceRing::inline_frame
+constexpr uint32_t kSvcInlineMax = 48;
+// Horner hash of the request's sequence number and the 12 dwords of the
+// inline frame (zero-padded to 48 bytes), mod 2^32
+__host__ __device__ inline uint32_t svc_inline_check(uint32_t seq, const uint32_t* d12) {
+  uint32_t h = seq;
+  for (int k = 0; k < 12; ++k) h = h * 0x9E3779B1u + d12[k];
+  return h;
+}
 constexpr uint32_t kSvcDesc = kSvcFrame + kSvcMaxFrame;
 constexpr uint32_t kSvcAns = kSvcDesc + 8 * kSvcMaxBurst;
 constexpr size_t kSvcBytes = kSvcAns + 8 * kSvcMaxBurst;
 static_assert(sizeof(ServiceRing) == 256, "two 128-byte lines");
-static_assert(offsetof(ServiceRing, req) == 0 && offsetof(ServiceRing, stop) == 8,
-              "the service polls req and stop with one 16-byte load");
+static_assert(offsetof(ServiceRing, req) == 0 && offsetof(ServiceRing, stop) == 8 &&
+                  offsetof(ServiceRing, check) == 12 && offsetof(ServiceRing, inline_frame) == 16,
+              "the service polls req, stop, check and the inline frame with one 64-byte load");
 
 struct ServiceArgs {
   ServiceRing* ring;  // device view of the host slot

@@ -787,6 +787,170 @@ constexpr uint32_t kMixedLut = kFixLut<3, MixedKeysL>;  // after the 4 combine s
 #endif
 using MixedLds = WindowLds<kMixedLut + 256u, RICRC_MIXED_WINDOW>;
 
+// The four-chain fold of the small kernel (and the ragged kernel's compact
+// tiny batches) over dwords [0, n) of one frame,
+// each dword through the per-dword masks of an IHL of `ihl` (IPv4 options,
+// malformed frames, the last batch read straight from global memory: frame at
+// `f`; else the frame staged in LDS at `pb`).  Out of line: its per-dword
+// mask constants are uniform values the hot loop would otherwise keep live
+// (they were ~200 SGPRs spilled to VGPR lanes in round 2, all in this path).
+template <bool GLOBAL, class K, uint32_t COMB>
+__device__ __forceinline__ uint32_t fold_masked4(const uint8_t* f, uint32_t pb, int ihl, int n) {
+  const K kk = K::make(__lane_id());
+  const int ns = (n + 3) >> 2, pad = 4 * ns - n;
+  uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+  for (int j = 0; j < ns; ++j) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = 4 * j + c - pad;
+      uint32_t w = 0;
+      if (k >= 0) w = fix_dword(GLOBAL ? ldg32(f + 4 * k) : lds_rd(pb + 4u * (uint32_t)k), k,
+                                ihl + 1, ihl + 3);
+      kk.absorb(P[c], T[c], w);
+    }
+  }
+  uint32_t R = mul_comb(P[3] ^ T[3], COMB) ^ P[2] ^ T[2];
+  R = mul_comb(R, COMB) ^ P[1] ^ T[1];
+  return mul_comb(R, COMB) ^ P[0] ^ T[0];
+}
+template <bool GLOBAL, class K, uint32_t COMB>
+__device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb, int ihl, int n) {
+  return fold_masked4<GLOBAL, K, COMB>(f, pb, ihl, n);
+}
+
+// Compact tiny batches ("phase 0", round 4).  The responder's frames (ACK /
+// NAK / atomic ack, 48-56 B, src/roce_rq.py:767-853) come in packed runs: 64
+// consecutive window packets whose frames lie in order, without overlap,
+// inside one 4 KiB span.  Such a batch needs neither the sort nor a lane group:
+// the wave stages the span with 16-byte coalesced loads (4 per lane) into its
+// own LDS slot -- the window's sort arrays, not yet filled -- each lane patches
+// its frame's masked dwords and seed in place and folds the frame from LDS as
+// the small-frame kernel does (four Mul(128) chains, three Mul(-32) Horner
+// steps), and the next batch's span is in flight while this one folds.  The
+// descriptor pass finds the batches (one wave = 64 consecutive packets of one
+// descriptor round) and leaves them out of the sort.
+constexpr uint32_t kCompactSpan = 4096;                        // bytes one wave stages per batch
+constexpr int kCompactLoads = (int)(kCompactSpan / 16u / 64u);  // 16-byte loads per lane
+constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a batch may hold
+static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
+              "every wave's staging slot inside the sort arrays");
+// the window's compact batches: {span start (u64), batch index, span bytes}
+constexpr uint32_t kCompactList = MixedLds::kBytes;
+constexpr uint32_t kMixedLdsBytes = kCompactList + 16u * (uint32_t)(MixedLds::kWindow / 64);
+static_assert(kMixedLdsBytes <= 163840u, "LDS");
+
+template <bool VERIFY>
+__device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, int cnt, int ncb,
+                                                int wave, int lane, uint32_t ok_lds) {
+  const MixedKeysS kk = MixedKeysS::make(lane);  // Mul(128) is staged in the G = 4 half
+  constexpr uint32_t kComb = MixedKeysS::kComb;   // Mul(-32)
+  const uint32_t slot = MixedLds::kPerm + (uint32_t)wave * kCompactSpan;
+  struct Ent {
+    uint64_t b16;
+    uint32_t bi, span;
+  };
+  auto entry = [&](int k) {
+    const u32x4 v = *(const lds_u32x4*)(uintptr_t)(kCompactList + 16u * (uint32_t)k);
+    Ent e;
+    e.b16 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.x) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.y) << 32);
+    e.bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
+    e.span = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
+    return e;
+  };
+  // a batch's span chunks and its lanes' descriptors (unconditional, clamped)
+  auto load = [&](int k, u32x4* X, uint32_t& L, uint64_t& O) {
+    const Ent e = entry(k);
+    const uint32_t last = (e.span + 15u) / 16u - 1u;
+    const uint8_t* base = (const uint8_t*)(uintptr_t)e.b16;
+#pragma unroll
+    for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
+    const uint32_t i = min(e.bi * 64u + (uint32_t)lane, (uint32_t)cnt - 1u);
+    L = a.lens[w0 + i];
+    O = a.offsets[w0 + i];
+  };
+  int k = wave;
+  if (k >= ncb) return;
+  u32x4 X[kCompactLoads];
+  uint32_t Ln;
+  uint64_t On;
+  load(k, X, Ln, On);
+  for (; k < ncb; k += kIcrcWaves) {
+    const Ent e = entry(k);
+    const uint32_t last = (e.span + 15u) / 16u - 1u;
+    body_prio_hi();
+#pragma unroll
+    for (int t = 0; t < kCompactLoads; ++t)
+      *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
+    __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
+    const uint32_t L = Ln;
+    const uint64_t O = On;
+    load(min(k + kIcrcWaves, ncb - 1), X, Ln, On);  // the next batch, in flight during the fold
+    body_prio_lo();
+    const uint32_t i = e.bi * 64u + (uint32_t)lane;
+    const bool live = i < (uint32_t)cnt;
+    const uint32_t pb = slot + (uint32_t)((uint64_t)(uintptr_t)(a.frames + O) - e.b16);
+    const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the descriptor pass checked every lane)
+    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+    const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
+    uint32_t st = 0;
+    const int ihl = (int)(d0 & 0xFu);
+    if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
+      st |= kPktNotIpv4;
+    else if (((d2 >> 8) & 0xFFu) != 17u)
+      st |= kPktNotUdp;
+    else if (L < (uint32_t)(4 * ihl + 24))
+      st |= kPktBadLen;
+    if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
+    const bool good = (st & kPktFatal) == 0;
+    uint32_t R;
+    if (__all(good && ihl == 5)) {
+      // every frame IHL 5: masks and seed patched in place, then the four
+      // chains with the lane's own zero pad in front (absorbing zeros into a
+      // zero register keeps it zero, so shorter frames just start later)
+      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+      __asm__ __volatile__("" ::: "memory");
+      int nsm = (n + 3) >> 2;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+      const int ns = __builtin_amdgcn_readfirstlane(nsm);
+      const int pad = 4 * ns - n;
+      const uint32_t pz = pb - 4u * (uint32_t)pad;
+      uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
+        if (j < ns) {  // uniform
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int kp = 4 * j + c;
+            const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
+            kk.absorb(P[c], T[c], kp >= pad ? w : 0u);
+          }
+        }
+      }
+      R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
+      R = mul_comb(R, kComb) ^ P[1] ^ T[1];
+      R = mul_comb(R, kComb) ^ P[0] ^ T[0];
+    } else {
+      R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
+    }
+    const uint32_t icrc = good ? ~R : 0u;
+    if (live) {
+      if constexpr (VERIFY) {
+        const bool ok = good && trailer == icrc;
+        if (good && !ok) st |= kPktIcrcMismatch;
+        lds_wr8(ok_lds + i, ok ? 1u : 0u);
+      }
+      if (a.icrc_out) stg32<kPktStorePol>(a.icrc_out + w0 + i, icrc);
+      if (a.status_out) stg8<kPktStorePol>(a.status_out + w0 + i, st);
+    }
+    __asm__ __volatile__("" ::: "memory");
+  }
+}
+
 template <int LOG2G, bool VERIFY, class K>
 __device__ __forceinline__ void mixed_set(const IcrcArgs& a, int s, int e, uint32_t w0, int lane,
                                           const OutBuf& ob) {
@@ -838,7 +1002,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   constexpr uint32_t kNoOff = 0xFFFFFFFFu;
   lds_u32* claim = (lds_u32*)(uintptr_t)(LD::kBase - 4u);  // (free words at the end of the LUT)
   lds_u32* tclaim = (lds_u32*)(uintptr_t)(LD::kBase - 8u);  // phase A's claim counter
+  lds_u32* ncompact = (lds_u32*)(uintptr_t)(LD::kBase - 12u);  // phase 0: batches listed
+  lds_u32* ncompact_pkts = (lds_u32*)(uintptr_t)(LD::kBase - 16u);  // ... and their packets
   const bool from_back = ((tid >> 6) & 1) != 0;
+  const int wave = tid >> 6;
   bool s_tiny = false;  // (uniform) the G = 4 half holds Mul(128) instead of Mul(512)
 
   const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
@@ -848,6 +1015,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     if (tid < NB) hist[tid] = 0;
     if (tid == NB) *claim = 0;
     if (tid == NB + 1) *tclaim = 0;
+    if (tid == NB + 2) *ncompact = 0;
+    if (tid == NB + 3) *ncompact_pkts = 0;
     __syncthreads();
     constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
     int keys[KR];
@@ -862,13 +1031,14 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       Lr[r] = a.lens[w0 + ic];
       Or[r] = a.offsets[w0 + ic];
     }
-#pragma unroll
-    for (int r = 0; r < KR; ++r) {
+    // sort key, offset / 4 and length of window packet i (key -1: a compact
+    // batch's packet, left out of the sort)
+    auto describe_key = [&](int r, bool compact) {
       const int i = tid + r * kIcrcThreads;
       int key = 0;
       offw[r] = kNoOff;
       lw[r] = 0;
-      if (i < cnt) {
+      if (i < cnt && !compact) {
         const uint32_t L = Lr[r];
         const uint64_t off = Or[r];
         if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
@@ -878,11 +1048,71 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
           // bucket 0: tiny frames (and unusable ones, which cost nothing)
           key = L <= kTinyLen ? 0 : min(NB - 1, 1 + (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
         }
-        atomicAdd((uint32_t*)&hist[key], 1u);
       }
-      keys[r] = key;
+      keys[r] = compact ? -1 : key;
+      return i < cnt && !compact;
+    };
+    // Phase 0's test, per descriptor round (wave-uniform: the wave's 64
+    // packets of the round): every live frame tiny, dword-aligned, after its
+    // left neighbour's end, and inside the 4 KiB from the first frame's
+    // 16-byte line.
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      bool compact = false;
+      if (r * kIcrcThreads + wave * 64 < cnt) {  // (uniform) lane 0 is live
+        const bool live = tid + r * kIcrcThreads < cnt;
+        const uint32_t L = Lr[r];
+        const uint64_t addr = (uint64_t)(uintptr_t)(a.frames + Or[r]);
+        const uint64_t b16 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr >> 32))
+                               << 32)) & ~15ull;
+        const uint64_t end = addr + L;
+        const uint64_t prev_end =
+            (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)end, 1, 64) |
+            ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(end >> 32), 1, 64) << 32);
+        const bool ok = !live || (L >= 44 && L <= kCompactMaxLen && (L & 3u) == 0 && (addr & 3u) == 0 &&
+                                  addr >= b16 && end <= b16 + kCompactSpan &&
+                                  (lane == 0 || addr >= prev_end));
+        compact = __all(ok);
+        if (compact) {
+          uint32_t span = live ? (uint32_t)(end - b16) : 0u;
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) span = max(span, (uint32_t)__shfl_xor((int)span, d, 64));
+          const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
+          if (lane == 0) {
+            const uint32_t slot = atomicAdd((uint32_t*)ncompact, 1u);
+            // (an opaque batch index: as a constant the compiler kept one
+            // 16-byte entry template per round live across the window loop)
+            uint32_t bid = (uint32_t)(r * kIcrcWaves + wave);
+            asm volatile("" : "+v"(bid));
+            *(lds_u32x4*)(uintptr_t)(kCompactList + 16u * slot) =
+                u32x4{(uint32_t)b16, (uint32_t)(b16 >> 32), bid, span};
+            atomicAdd((uint32_t*)ncompact_pkts, nlive);
+          }
+        }
+      }
+      if (describe_key(r, compact)) atomicAdd((uint32_t*)&hist[keys[r]], 1u);
     }
     __syncthreads();
+    OutBuf ob = {0, 0};
+    if constexpr (VERIFY) {
+      ob.ok_p0 = w0;
+      ob.ok_cap = (uint32_t)cnt;
+      ob.ok_lds = LD::kOk;
+    }
+    // ---- phase 0: the compact tiny batches, before the sort fills the arrays
+    // their waves stage through; the rest of the window (cs packets) is sorted
+    const int ncb = (int)__builtin_amdgcn_readfirstlane((int)*ncompact);
+    const int cs = cnt - (int)__builtin_amdgcn_readfirstlane((int)*ncompact_pkts);
+    if (ncb > 0) {
+      if (!s_tiny) {
+        MixedKeysS::template stage<kIcrcThreads>(a.tables + 0 * 1024, tid);  // main set 0: Mul(128)
+        s_tiny = true;
+        __syncthreads();
+      }
+      compact_batches<VERIFY>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+      __syncthreads();  // the staging slots are the sort arrays again
+    }
     // (uniform) the window's tiny frames, sorted to its front
     const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
     const int ntiny = ntiny_all >= kTinyMin ? ntiny_all : 0;
@@ -903,7 +1133,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int i = tid + r * kIcrcThreads;
-      if (i < cnt) {
+      if (i < cnt && keys[r] >= 0) {
         const uint32_t pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
         perm[pos] = (uint16_t)i;
         roff[pos] = offw[r];
@@ -911,12 +1141,6 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       }
     }
     __syncthreads();
-    OutBuf ob = {0, 0};
-    if constexpr (VERIFY) {
-      ob.ok_p0 = w0;
-      ob.ok_cap = (uint32_t)cnt;
-      ob.ok_lds = LD::kOk;
-    }
     // ---- phase A: the tiny prefix [0, ntiny) as G = 1 sets of 64 packets,
     // claimed from both ends, with Mul(128) in the Keys8 rows' G = 4 half
     if (ntiny > 0) {
@@ -937,21 +1161,21 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       }
       __syncthreads();  // phase A done before its table is replaced
     }
-    if (ntiny < cnt && s_tiny) {  // (uniform) phase B needs Mul(512) back
+    if (ntiny < cs && s_tiny) {  // (uniform) phase B needs Mul(512) back
       MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
       s_tiny = false;
       __syncthreads();
     }
-    // ---- phase B: [ntiny, cnt) as G = 4 / G = 8 sets (below), claims
+    // ---- phase B: [ntiny, cs) as G = 4 / G = 8 sets (below), claims
     // counted from ntiny
-    const int nb = cnt - ntiny;
+    const int nb = cs - ntiny;
     // Claim size: 16 packets while the frames at this wave's end of the window
     // are short, else 8.  Decided from the window's first 16 / last frame, then
     // from the wave's own previous claim (the front end only grows longer, the
     // back end only shorter), so a claim costs one LDS atomic.
     uint32_t size = nb <= 0 ? 8u
                     : (uint32_t)__builtin_amdgcn_readfirstlane(
-                          (int)rlen[from_back ? cnt - 1 : ntiny + min(15, nb - 1)]) <= kMixedShortLen
+                          (int)rlen[from_back ? cs - 1 : ntiny + min(15, nb - 1)]) <= kMixedShortLen
                         ? 16u : 8u;
     for (;;) {
       uint32_t old = 0;
@@ -963,11 +1187,11 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       // G = 4 set if the longest (sorted last) is short, else as G = 8 sets of 8
       int s, e;
       if (from_back) {
-        e = cnt - bk;
+        e = cs - bk;
         s = max(e - (int)size, ntiny + f);
       } else {
         s = ntiny + f;
-        e = min(ntiny + f + (int)size, cnt - bk);
+        e = min(ntiny + f + (int)size, cs - bk);
       }
       if (size == 16u) {
         const uint32_t longest = (uint32_t)__builtin_amdgcn_readfirstlane((int)rlen[e - 1]);
@@ -1072,32 +1296,6 @@ constexpr int kSmallOutRounds = RICRC_SMALL_OUTBUF;  // output ring depth in rou
 #define RICRC_SMALL_OUT_POL 16
 #endif
 constexpr int kSmallOutPol = RICRC_SMALL_OUT_POL;
-
-// The four-chain fold of the small kernel over dwords [0, n) of one frame,
-// each dword through the per-dword masks of an IHL of `ihl` (IPv4 options,
-// malformed frames, the last batch read straight from global memory: frame at
-// `f`; else the frame staged in LDS at `pb`).  Out of line: its per-dword
-// mask constants are uniform values the hot loop would otherwise keep live
-// (they were ~200 SGPRs spilled to VGPR lanes in round 2, all in this path).
-template <bool GLOBAL>
-__device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb, int ihl, int n) {
-  const SmallKeys kk = SmallKeys::make(__lane_id());
-  const int ns = (n + 3) >> 2, pad = 4 * ns - n;
-  uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
-  for (int j = 0; j < ns; ++j) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = 4 * j + c - pad;
-      uint32_t w = 0;
-      if (k >= 0) w = fix_dword(GLOBAL ? ldg32(f + 4 * k) : lds_rd(pb + 4u * (uint32_t)k), k,
-                                ihl + 1, ihl + 3);
-      kk.absorb(P[c], T[c], w);
-    }
-  }
-  uint32_t R = mul_comb(P[3] ^ T[3], kSmallComb) ^ P[2] ^ T[2];
-  R = mul_comb(R, kSmallComb) ^ P[1] ^ T[1];
-  return mul_comb(R, kSmallComb) ^ P[0] ^ T[0];
-}
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
@@ -1248,7 +1446,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
       R = fold4([&](int, int kp) { return lds_rd(pz + 4u * (uint32_t)kp); });
     } else {
-      R = small_fold_masked<false>(nullptr, pb, ihl, n);
+      R = small_fold_masked<false, SmallKeys, kSmallComb>(nullptr, pb, ihl, n);
     }
     emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing && to_ring);
     __asm__ __volatile__("" ::: "memory");
@@ -1348,7 +1546,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
     int ihl;
     const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
-    const uint32_t R = small_fold_masked<true>(f, 0u, ihl, n);
+    const uint32_t R = small_fold_masked<true, SmallKeys, kSmallComb>(f, 0u, ihl, n);
     emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
   }
 }
@@ -1512,7 +1710,7 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   a.icrc_out = (uint32_t*)(lds_u32*)(uintptr_t)kOut;
   a.status_out = (uint8_t*)(lds_u32*)(uintptr_t)(kOut + 4u);
   uint32_t served = s.served;
-  const auto ring_rsrc = out_rsrc(r, 16u);
+  const auto ring_rsrc = out_rsrc(r, 64u);
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   uint32_t polls = 0;
   // one poll's value: 0 = nothing to do, 1 = a request served, 2 = leave
@@ -1525,7 +1723,48 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
     if (seq != served) {
       const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before req
-      const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(req >> 32));
+      uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(req >> 32));
+      bool inl = false;
+      if (L & kSvcInline) {  // (uniform) the 48 bytes of lanes 1-3 against the check word
+        uint32_t d12[12];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          d12[4 * q + 0] = (uint32_t)__builtin_amdgcn_readlane((int)head.x, q + 1);
+          d12[4 * q + 1] = (uint32_t)__builtin_amdgcn_readlane((int)head.y, q + 1);
+          d12[4 * q + 2] = (uint32_t)__builtin_amdgcn_readlane((int)head.z, q + 1);
+          d12[4 * q + 3] = (uint32_t)__builtin_amdgcn_readlane((int)head.w, q + 1);
+        }
+        inl = (uint32_t)__builtin_amdgcn_readfirstlane((int)head.w) == svc_inline_check(seq, d12) &&
+              (L & ~kSvcInline) <= kSvcInlineMax;
+      }
+      if (inl) {
+        // the frame came with the poll (lanes 1-3 hold its 48 bytes): into LDS,
+        // then folded from there as a one-frame burst on this wave (G = 8)
+        L &= ~kSvcInline;
+        if (lane >= 1 && lane <= 3) *(lds_u32x4*)(uintptr_t)(kBurstStage + 16u * (uint32_t)(lane - 1)) = head;
+        if (lane == 0)
+          *(__attribute__((address_space(3))) uint64_t*)(uintptr_t)kSvcDescLds = (uint64_t)L << 32;
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // (lgkmcnt(0): the frame and descriptor are in LDS)
+        __asm__ __volatile__("" ::: "memory");
+        serve_burst<false>(1u, lane, 0);
+        __asm__ __volatile__("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0);  // the result's flat stores have landed
+        __asm__ __volatile__("" ::: "memory");
+        if (lane == 0) {
+          const uint64_t ans = (uint64_t)lds_rd(kBurstIcrc) | ((uint64_t)lds_rd8(kBurstSt) << 32) |
+                               ((uint64_t)(seq & kSvcSeqMask) << 40);
+          r->t_seen = t_seen;
+          r->t_done = __builtin_amdgcn_s_memrealtime();
+          r->polls = polls;
+          __hip_atomic_store(&r->resp, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        polls = 0;
+        served = seq;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        return 1;
+      }
+      L &= ~kSvcInline;  // (a torn inline read: the frame at kSvcFrame, below)
       if (L & kSvcBurst) {
         const uint32_t cnt = min(L & 0xFFu, kSvcMaxBurst);
         const uint32_t kib = min((L >> 16) & 0x7Fu, kSvcMaxFrame / 1024u);  // packed KiB
@@ -1634,7 +1873,10 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   // a request is seen about half a round trip sooner.  A poll issued before a
   // request was served shows its sequence number again (== served): ignored.
   // The busy word is read beside the slot (both loads in flight together).
-  auto poll = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, 0u, 0u, 17); };
+  // (lanes 0-3 read the slot's first 64 bytes: request, stop, check and the
+  // inline frame; the other lanes repeat lane 3's chunk -- one 64-byte read)
+  const uint32_t poll_off = 16u * (uint32_t)min(lane, 3);
+  auto poll = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, poll_off, 0u, 17); };
   auto poll_busy = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(busy_rsrc, 0u, 0u, 17); };
   u32x4 hA = poll(), bA = poll_busy();
   for (;;) {
@@ -1682,7 +1924,7 @@ size_t lds_bytes(int log2g, bool ragged) {
     case 0: return RaggedLds<0>::kBytes;
     case 1: return RaggedLds<1>::kBytes;
     case 2: return RaggedLds<2>::kBytes;
-    case 3: return RICRC_RAGGED_MIXED ? MixedLds::kBytes : RaggedLds<3>::kBytes;
+    case 3: return RICRC_RAGGED_MIXED ? kMixedLdsBytes : RaggedLds<3>::kBytes;
     case 4: return RaggedLds<4>::kBytes;
     case 5: return RaggedLds<5>::kBytes;
     default: return RaggedLds<6>::kBytes;

@@ -399,3 +399,33 @@ def test_process_exit_after_context_free_calls_on_threads():
     assert r.returncode == 0, r.stderr[-2000:]
     assert "answered" in r.stdout
     assert time.perf_counter() - t0 < 60
+
+
+def test_inline_requests_for_ack_sized_frames(engine):
+    """Round 4: a frame of at most 48 bytes rides in the slot's first 64
+    bytes (read by the wave's poll with the request word, guarded by a check
+    word).  Every length 0..52 around that bound -- ACK (48), NAK, bare BTH
+    (44), odd lengths, too-short frames, malformed headers -- back to back and
+    interleaved with larger frames, against the reference's rule."""
+    engine.set_service(1000)
+    ack = o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x11, psn=9), ext=o.aeth_bytes(0, 31, 4))
+    assert len(ack) == 48
+    rng = np.random.default_rng(17)
+    frames = []
+    for L in range(0, 53):
+        f = bytearray(ack[:L] if L <= 48 else ack + bytes(L - 48))
+        if len(f) >= 4:
+            f[2:4] = L.to_bytes(2, "big")
+        frames.append(bytes(f))
+    for i in range(400):  # ACKs differing in PSN and MSN only (the common stream)
+        f = o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x11, psn=i), ext=o.aeth_bytes(0, 31, i))
+        frames.append(f)
+        if i % 50 == 0:
+            frames.append(bytes(rng.integers(0, 256, 48, dtype=np.uint8)))  # garbage
+            frames.append(_frames()[i % 8])                                  # a larger frame
+    for f in frames:
+        icrc, st = engine.compute_one(f)
+        assert icrc == _want(f), (len(f), hex(icrc), hex(_want(f)), st)
+    from roce_icrc.engine import icrc as free_icrc
+    for f in frames[:60]:
+        assert free_icrc(f)[0] == _want(f)

@@ -103,3 +103,116 @@ def test_window_sequences_switch_the_table_half(engine):
     want, _ = oracle_batch(buf, offs, lens)
     got, _ = _run(engine, buf, offs, lens)
     np.testing.assert_array_equal(got, want)
+
+
+def _dev_compute(engine, buf, offs, lens):
+    """compute_batch_dev with status: (icrc, status) as numpy."""
+    torch = pytest.importorskip("torch")
+    n = lens.size
+    d = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.compute_batch_dev(d, do, dl, n, out, st)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32).copy(), st.cpu().numpy().copy()
+
+
+def test_compact_ack_batches(engine):
+    """Phase 0 (round 4): packed runs of ACK-sized frames (64 consecutive
+    packets in order inside 4 KiB) are staged and folded lane-per-packet
+    without the sort.  All-ACK batches with a partial last batch and several
+    windows per workgroup, plus 44-64 B mixes; compute and verify (corrupted
+    trailers and payloads flagged) against the oracle."""
+    rng = np.random.default_rng(21)
+    for n, choices in ((100003, [48]), (1 << 22, [48]), (300001, [44, 48, 52, 56, 60, 64])):
+        lens = rng.choice(choices, n).astype(np.uint32)
+        buf, offs, lens = _ragged(lens, n % 1000)
+        want, _ = oracle_batch(buf, offs, lens)
+        got, (ok, bad) = _run(engine, buf, offs, lens, verify=True, flip_every=89)
+        np.testing.assert_array_equal(got, want, err_msg=f"n {n}")
+        expect = np.ones(n, bool)
+        expect[bad] = False
+        np.testing.assert_array_equal(ok, expect, err_msg=f"n {n}")
+
+
+def test_compact_batches_malformed_and_options(engine):
+    """Frames inside compact batches that leave the IHL-5 fast path: IPv4
+    options (IHL 6), not IPv4, not UDP, a wrong IP total length.  ICRC words
+    against the oracle and status bits against the lane-group kernel (an
+    explicit lanes setting never takes phase 0) on the same frames."""
+    from roce_icrc import IcrcEngine
+    import icrc_oracle as o  # checker only
+    n = 64 * 300 + 17
+    rng = np.random.default_rng(5)
+    lens = np.full(n, 48, np.uint32)
+    frames = []
+    for i in range(n):
+        if i % 97 == 5:  # IHL 6: one option dword, 52 B
+            f = bytearray(o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x11, psn=i),
+                                        ext=o.aeth_bytes()))
+            f = f[:20] + bytearray(b"\x01\x01\x01\x01") + f[20:]
+            f[0] = 0x46
+            tot = len(f)
+            f[2:4] = tot.to_bytes(2, "big")
+            frames.append(bytes(f))
+            continue
+        f = bytearray(o.build_frame("10.0.0.1", "10.0.0.2", 7, dict(opcode=0x11, psn=i),
+                                    ext=o.aeth_bytes()))
+        if i % 89 == 3:
+            f[0] = 0x65           # not IPv4
+        elif i % 83 == 7:
+            f[9] = 6              # TCP
+        elif i % 79 == 1:
+            f[3] ^= 4             # IP total length mismatch
+        f[-4:] = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+        frames.append(bytes(f))
+    from roce_icrc import pack_aligned
+    buf, offs, lens = pack_aligned(frames)
+    want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
+    got, st = _dev_compute(engine, buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+    e8 = IcrcEngine(0, lanes=8)
+    try:
+        got8, st8 = _dev_compute(e8, buf, offs, lens)
+    finally:
+        e8.close()
+    np.testing.assert_array_equal(got8, want)
+    np.testing.assert_array_equal(st, st8)
+    assert (st != 0).sum() > 100
+
+
+def test_compact_test_rejects_unsafe_layouts(engine):
+    """Batches phase 0 must NOT take (they go through the sort, still exact):
+    frames in reverse order, the same frame twice (in-place masks would be
+    applied twice), a gap that stretches the span past 4 KiB, frames at
+    2-byte offsets, and frames longer than 128 B between tiny ones."""
+    rng = np.random.default_rng(8)
+    n = 64 * 64
+    lens = np.full(n, 48, np.uint32)
+    buf, offs, lens = _ragged(lens, 4)
+    offs = offs.copy()
+    b = lambda k: slice(64 * k, 64 * k + 64)  # noqa: E731
+    offs[b(1)] = offs[b(1)][::-1].copy()                      # reversed
+    offs[b(2)][10] = offs[b(2)][9]                            # duplicate frame
+    offs[b(3)][32:] += 4096                                   # gap: span > 4 KiB
+    big = np.zeros(buf.size + 8192 + 4096, np.uint8)
+    big[:buf.size] = buf
+    buf = big
+    # 2-byte-offset copy of batch 4's frames at the end of the buffer
+    src = offs[b(4)].astype(np.int64)
+    dst = buf.size - 4096 + 2 + 48 * np.arange(64)
+    for s_, d_ in zip(src, dst):
+        buf[d_:d_ + 48] = buf[s_:s_ + 48]
+    offs[b(4)] = dst.astype(np.uint64)
+    want, _ = oracle_batch(buf, offs, lens)
+    got, _ = _dev_compute(engine, buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+    # a 300-B frame between ACKs: that batch is not compact, its neighbours are
+    lens2 = np.full(n, 48, np.uint32)
+    lens2[64 * 5 + 7] = 300
+    buf2, offs2, lens2 = _ragged(lens2, 6)
+    want2, _ = oracle_batch(buf2, offs2, lens2)
+    got2, _ = _dev_compute(engine, buf2, offs2, lens2)
+    np.testing.assert_array_equal(got2, want2)
