@@ -794,6 +794,28 @@ using MixedLds = WindowLds<kMixedLut + 256u, RICRC_MIXED_WINDOW>;
 // `f`; else the frame staged in LDS at `pb`).  Out of line: its per-dword
 // mask constants are uniform values the hot loop would otherwise keep live
 // (they were ~200 SGPRs spilled to VGPR lanes in round 2, all in this path).
+// Mul(-32) for the four-chain folds: from the unreplicated combine set at LDS
+// address COMB, or (COMB == kComb8) from the 8-copy Keys8 layout in the high
+// halves of the table rows (conflict-free, one v_perm per address; the
+// selectors are those of the low-half keys).
+constexpr uint32_t kComb8 = 0xFFFFFFFFu;
+template <uint32_t COMB, class K>
+__device__ __forceinline__ uint32_t comb4(uint32_t x, const K& kk) {
+  if constexpr (COMB == kComb8) {
+    Keys8T<1> kc;
+    kc.k = kk.k | 0x80808080u;
+    kc.s0 = kk.s0;
+    kc.s1 = kk.s1;
+    kc.s2 = kk.s2;
+    kc.s3 = kk.s3;
+    uint32_t P = 0, T = 0;
+    kc.absorb(P, T, x);
+    return P ^ T;
+  } else {
+    return mul_comb(x, COMB);
+  }
+}
+
 template <bool GLOBAL, class K, uint32_t COMB>
 __device__ __forceinline__ uint32_t fold_masked4(const uint8_t* f, uint32_t pb, int ihl, int n) {
   const K kk = K::make(__lane_id());
@@ -809,9 +831,9 @@ __device__ __forceinline__ uint32_t fold_masked4(const uint8_t* f, uint32_t pb, 
       kk.absorb(P[c], T[c], w);
     }
   }
-  uint32_t R = mul_comb(P[3] ^ T[3], COMB) ^ P[2] ^ T[2];
-  R = mul_comb(R, COMB) ^ P[1] ^ T[1];
-  return mul_comb(R, COMB) ^ P[0] ^ T[0];
+  uint32_t R = comb4<COMB>(P[3] ^ T[3], kk) ^ P[2] ^ T[2];
+  R = comb4<COMB>(R, kk) ^ P[1] ^ T[1];
+  return comb4<COMB>(R, kk) ^ P[0] ^ T[0];
 }
 template <bool GLOBAL, class K, uint32_t COMB>
 __device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb, int ihl, int n) {
@@ -1265,9 +1287,19 @@ constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
 #endif
 constexpr uint32_t kSmallTailDiv = RICRC_SMALL_TAIL_DIV;
 using SmallKeys = Keys8;
-constexpr uint32_t kSmallComb = 163840u - 4096u;
+// Mul(-32) for the combine: unreplicated in the last 4 KiB, or (SMALL_COMB8)
+// as 8 conflict-free copies in the high halves of the table rows, the output
+// ring then entirely after the staging slots
+#ifndef RICRC_SMALL_COMB8
+#define RICRC_SMALL_COMB8 0
+#endif
+constexpr bool kSmallComb8 = RICRC_SMALL_COMB8 != 0;
+constexpr uint32_t kSmallCombLds = 163840u - 4096u;
+constexpr uint32_t kSmallComb = kSmallComb8 ? kComb8 : kSmallCombLds;
+constexpr uint32_t kSmallEnd = kSmallComb8 ? 163840u : kSmallCombLds;  // end of the staging + ring tail
 constexpr uint32_t kSmallStage = 65536;
-constexpr uint32_t kSmallHoleWords = 256u * (256u - Keys8::kHole) / 4u;  // ring words in the row halves
+constexpr uint32_t kSmallHoleWords =
+    kSmallComb8 ? 0u : 256u * (256u - Keys8::kHole) / 4u;  // ring words in the row halves
 // LDS byte address of ring word k / ring quad i (16 B): the row halves first,
 // then the tail after the staging slots
 __device__ __forceinline__ uint32_t small_ring_word(uint32_t tail, uint32_t k) {
@@ -1312,7 +1344,14 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m128[w]);
     }
     const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
-    for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallComb + 4u * i, cm32[i]);
+    if constexpr (kSmallComb8) {
+      for (int i = tid; i < 2048; i += (int)blockDim.x) {
+        const int w = i >> 1, h = i & 1;
+        lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128), cm32[w]);
+      }
+    } else {
+      for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallCombLds + 4u * i, cm32[i]);
+    }
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
@@ -1349,7 +1388,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   constexpr bool kRing = kSmallOutRounds > 0 && (OUTS & 1) != 0 && !VERIFY;
   const uint32_t ring = kSmallStage + nw * 64u * S;  // the ring's tail (small_ring_word)
   const uint32_t rounds_cap =
-      kRing ? min((uint32_t)kSmallOutRounds, (kSmallHoleWords + (kSmallComb - ring) / 4u) / (nw * 64u)) : 0u;
+      kRing ? min((uint32_t)kSmallOutRounds, (kSmallHoleWords + (kSmallEnd - ring) / 4u) / (nw * 64u)) : 0u;
   uint32_t ring_base = 0;  // first packet of the ring's current window
   auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer,
                   bool to_ring = false) {
@@ -1386,9 +1425,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
         }
       }
     }
-    uint32_t R = mul_comb(P[3] ^ T[3], kSmallComb) ^ P[2] ^ T[2];
-    R = mul_comb(R, kSmallComb) ^ P[1] ^ T[1];
-    return mul_comb(R, kSmallComb) ^ P[0] ^ T[0];
+    uint32_t R = comb4<kSmallComb>(P[3] ^ T[3], kk) ^ P[2] ^ T[2];
+    R = comb4<kSmallComb>(R, kk) ^ P[1] ^ T[1];
+    return comb4<kSmallComb>(R, kk) ^ P[0] ^ T[0];
   };
   // per-dword masks (IPv4 options, the direct path, malformed frames)
 
@@ -2014,7 +2053,7 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
   kernel_fn k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;
-  uint32_t nw = min((uint32_t)kSmallMaxWaves, (kSmallComb - kSmallStage) / slot);
+  uint32_t nw = min((uint32_t)kSmallMaxWaves, (kSmallEnd - kSmallStage) / slot);
   if (nw > 2 && (nw & 1u)) --nw;  // even: every SIMD the same number of waves
   const size_t lds = 163840;  // staging slots, then the output ring in what is left
   const uint64_t nb = (a.n + 63) / 64;
