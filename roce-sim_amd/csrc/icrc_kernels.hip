@@ -1641,6 +1641,11 @@ __global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4
 // after `idle_ticks` of the 100 MHz real-time counter without a request:
 // every path through the loop reaches one of the two, so the grid always
 // drains; the host relaunches it on the next call.
+// Polls of the request slot in flight at once (2 or 4; A/B switch).
+#ifndef RICRC_SVC_POLLS
+#define RICRC_SVC_POLLS 2
+#endif
+constexpr int kSvcPolls = RICRC_SVC_POLLS;
 constexpr int kSvcThreads = 512;  // all stage the tables; wave 0 serves, waves 1-7 help with bursts
 constexpr int kSvcWaves = kSvcThreads / 64;
 // LDS of the service (round 3): Mul(8192) for single frames (G = 64) and
@@ -1917,15 +1922,36 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   const uint32_t poll_off = 16u * (uint32_t)min(lane, 3);
   auto poll = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, poll_off, 0u, 17); };
   auto poll_busy = [&]() { return __builtin_amdgcn_raw_buffer_load_b128(busy_rsrc, 0u, 0u, 17); };
-  u32x4 hA = poll(), bA = poll_busy();
-  for (;;) {
-    const u32x4 hB = poll(), bB = poll_busy();
-    ++polls;
-    if (step(hA, bA) == 2) break;
-    hA = poll();
-    bA = poll_busy();
-    ++polls;
-    if (step(hB, bB) == 2) break;
+  if constexpr (kSvcPolls == 4) {  // four polls in flight
+    u32x4 hA = poll(), bA = poll_busy(), hB = poll(), bB = poll_busy(), hC = poll(), bC = poll_busy();
+    for (;;) {
+      const u32x4 hD = poll(), bD = poll_busy();
+      ++polls;
+      if (step(hA, bA) == 2) break;
+      hA = poll();
+      bA = poll_busy();
+      ++polls;
+      if (step(hB, bB) == 2) break;
+      hB = poll();
+      bB = poll_busy();
+      ++polls;
+      if (step(hC, bC) == 2) break;
+      hC = poll();
+      bC = poll_busy();
+      ++polls;
+      if (step(hD, bD) == 2) break;
+    }
+  } else {
+    u32x4 hA = poll(), bA = poll_busy();
+    for (;;) {
+      const u32x4 hB = poll(), bB = poll_busy();
+      ++polls;
+      if (step(hA, bA) == 2) break;
+      hA = poll();
+      bA = poll_busy();
+      ++polls;
+      if (step(hB, bB) == 2) break;
+    }
   }
   __builtin_amdgcn_s_waitcnt(0);  // the poll still in flight has returned
   if (lane == 0)  // the helper waves leave too

@@ -580,6 +580,25 @@ def verify_frames(frames: list[bytes]) -> np.ndarray:
     return ok
 
 
+def multi_device_verifier(engines):
+    """A ``verify`` for ``RecvLoop`` on a node of several GPUs: each received
+    batch is split round robin over ``engines`` (one per device, frame i on
+    engines[i % len]) by ONE ricrc_verify_batch_multi call -- the receive side
+    of the per-packet independence the emit side shards on
+    (src/roce.py:192-219; the batch is what RoCEv2.recv_pkts,
+    src/roce_v2.py:327-372, would take from its socket)."""
+    from .engine import verify_batch_multi
+    engines = list(engines)
+    if not engines:
+        raise ValueError("multi_device_verifier needs at least one engine")
+
+    def verify(frames: list[bytes]) -> np.ndarray:
+        buf, offs, lens = pack_aligned(frames)
+        ok, _, _ = verify_batch_multi(engines, buf, offs, lens)
+        return ok
+    return verify
+
+
 def recv_datagrams(datagrams: list[bytes], qpn: Optional[int] = None):
     """Receive side for raw IPv4 datagrams (e.g. from an AF_INET/SOCK_RAW UDP
     socket): verify every ICRC in one GPU call, drop the failures (as Linux

@@ -82,3 +82,26 @@ def test_gpu_recv_loop_raw_socket_loopback(engine):
     finally:
         sink.close()
         src.close()
+
+
+def test_gpu_recv_loop_multi_device_verifier(engine):
+    """RecvLoop with its batches split over several contexts
+    (roce.multi_device_verifier -> ricrc_verify_batch_multi): the same
+    deliveries and drops as the one-device loop.  On a one-GPU box the
+    contexts share device 0 (the split and the scatter are what is tested)."""
+    from roce_icrc import IcrcEngine
+    from roce_icrc.engine import device_count
+    R.set_engine(engine)
+    frames, bad = _burst(200)
+    good = [f for k, f in enumerate(frames) if k not in bad]
+    others = [IcrcEngine(d % device_count()) for d in range(1, 3)]
+    try:
+        loop = RV.RecvLoop(RV.ListSource(frames), batch=97, keep_dropped=True,
+                           verify=R.multi_device_verifier([engine] + others))
+        pk = loop.packets(len(good))
+        assert [bytes(b.build()) for b in pk] == [f[28:] for f in good]
+        assert loop.stats.icrc_dropped == len(bad)
+        assert sorted(loop.stats.dropped_frames) == sorted(frames[k] for k in bad)
+    finally:
+        for e in others:
+            e.close()
