@@ -23,7 +23,9 @@ step ragged_ab_r04a 600 python scripts/ragged_ab.py --rounds 2 scratch/libs/base
 gcc -std=c99 -O2 -Iinclude scripts/latency_c.c -Lroce-sim_amd/roce_icrc -l:libroceicrc.so \
   -Wl,-rpath,$PWD/roce-sim_amd/roce_icrc -o $O/latency_c || exit 1
 step latency_c_r04a 300 ./$O/latency_c
-step latency_c_polls4_r04a 300 env LD_LIBRARY_PATH=$PWD/scratch/libs/polls4 ./$O/latency_c
+gcc -std=c99 -O2 -Iinclude scripts/latency_c.c -Lscratch/libs/polls4 -l:libroceicrc.so \
+  -Wl,-rpath,$PWD/scratch/libs/polls4 -o $O/latency_c_polls4 || exit 1
+step latency_c_polls4_r04a 300 ./$O/latency_c_polls4
 step small_stage_r04a 120 ./scratch/small_stage
 step cfg5_ab_r04a 600 python scratch/bench_ab.py --workloads cfg5 --rounds 3 scratch/libs/compact.so scratch/libs/comb8.so scratch/libs/comb8w10.so
 step svc_r04a 300 python scripts/svc_contention.py
