@@ -1134,6 +1134,13 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       }
       compact_batches<VERIFY>(a, w0, cnt, ncb, wave, lane, LD::kOk);
       __syncthreads();  // the staging slots are the sort arrays again
+      if (cs == 0) {  // (uniform) a window of compact batches only: nothing to sort
+        if constexpr (VERIFY) {
+          // (the next window's barrier precedes its first verdict write)
+          for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
+        }
+        continue;
+      }
     }
     // (uniform) the window's tiny frames, sorted to its front
     const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
