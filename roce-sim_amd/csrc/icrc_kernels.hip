@@ -840,6 +840,12 @@ __device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb
   return fold_masked4<GLOBAL, K, COMB>(f, pb, ihl, n);
 }
 
+// Window sort: wave-aggregated histogram / scatter atomics (A/B switch).
+#ifndef RICRC_HIST_AGG
+#define RICRC_HIST_AGG 0
+#endif
+constexpr bool kHistAgg = RICRC_HIST_AGG != 0;
+
 // Compact tiny batches ("phase 0", round 4).  The responder's frames (ACK /
 // NAK / atomic ack, 48-56 B, src/roce_rq.py:767-853) come in packed runs: 64
 // consecutive window packets whose frames lie in order, without overlap,
@@ -1113,7 +1119,22 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
           }
         }
       }
-      if (describe_key(r, compact)) atomicAdd((uint32_t*)&hist[keys[r]], 1u);
+      const bool counted = describe_key(r, compact);
+      if constexpr (kHistAgg) {
+        // one LDS atomic per distinct key of the wave (a wave of one key --
+        // tiny frames, a homogeneous batch -- otherwise serialises 64 adds
+        // on one address)
+        uint64_t todo = __ballot(counted);
+        while (todo) {
+          const int lead = __ffsll((unsigned long long)todo) - 1;
+          const int k = __shfl(keys[r], lead, 64);
+          const uint64_t m = __ballot(counted && keys[r] == k);
+          if (lane == lead) atomicAdd((uint32_t*)&hist[k], (uint32_t)__popcll(m));
+          todo &= ~m;
+        }
+      } else if (counted) {
+        atomicAdd((uint32_t*)&hist[keys[r]], 1u);
+      }
     }
     __syncthreads();
     OutBuf ob = {0, 0};
@@ -1162,8 +1183,25 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int i = tid + r * kIcrcThreads;
-      if (i < cnt && keys[r] >= 0) {
-        const uint32_t pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
+      const bool placed = i < cnt && keys[r] >= 0;
+      uint32_t pos = 0;
+      if constexpr (kHistAgg) {  // one atomic per distinct key; lanes in order within it
+        uint64_t todo = __ballot(placed);
+        while (todo) {
+          const int lead = __ffsll((unsigned long long)todo) - 1;
+          const int k = __shfl(keys[r], lead, 64);
+          const uint64_t m = __ballot(placed && keys[r] == k);
+          uint32_t base = 0;
+          if (lane == lead) base = atomicAdd((uint32_t*)&hist[k], (uint32_t)__popcll(m));
+          base = (uint32_t)__shfl((int)base, lead, 64);
+          if ((m >> lane) & 1ull)
+            pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          todo &= ~m;
+        }
+      } else if (placed) {
+        pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
+      }
+      if (placed) {
         perm[pos] = (uint16_t)i;
         roff[pos] = offw[r];
         rlen[pos] = (uint16_t)lw[r];
