@@ -35,11 +35,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-// LDS: [slots: NW * NS * 7 KiB][ring: RING rounds * NW * 256 B]
-template <int MODE, int NW, int RING>
+// LDS: [tables: 32 KiB if LK][slots: NW * NS * 7 KiB][ring: RING rounds * NW * 256 B]
+//   mode 2 (round 4): ONE slot per wave filled by LDS-DMA; a round reads its
+//   lane's 27 frame dwords into VGPRs, then refills the slot with the next
+//   batch (in flight during the fold), then folds from the registers.
+//   LK: table lookups per dword emulating the fold (4 chains, conflict-free
+//   32-copy addressing); 0 = a plain XOR.
+template <int MODE, int NW, int RING, int LK = 0>
 __global__ void __launch_bounds__(64 * NW, 1) stage(const uint8_t* frames, uint32_t n, uint32_t* out) {
-  constexpr int NS = MODE == 0 ? 1 : 2;
-  constexpr uint32_t kRing = NW * NS * kSlot;
+  constexpr int NS = MODE == 1 ? 2 : 1;
+  constexpr uint32_t kTab = LK ? 32768u : 0u;
+  constexpr uint32_t kRing = kTab + NW * NS * kSlot;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nb = n / 64;
   const uint32_t per = (nb + gridDim.x - 1) / gridDim.x;
@@ -47,7 +53,21 @@ __global__ void __launch_bounds__(64 * NW, 1) stage(const uint8_t* frames, uint3
   const uint32_t nrounds = b1 > b0 ? (b1 - b0 + NW - 1) / NW : 0;
   const auto fr = rsrc(frames, (uint32_t)min<uint64_t>((uint64_t)n * S, 0xFFFFFFF0u));
   const auto orr = rsrc(out, n * 4u);
-  const uint32_t slot0 = (uint32_t)wave * NS * kSlot;
+  const uint32_t slot0 = kTab + (uint32_t)wave * NS * kSlot;
+  if constexpr (LK > 0) {  // table (byte e, copy c) = e * 128 + c * 4: any value
+    for (uint32_t i = tid; i < 8192u; i += NW * 64) *(lds_u32*)(uintptr_t)(4u * i) = i * 2654435761u;
+    __syncthreads();
+  }
+  const uint32_t kc = (uint32_t)(lane & 31) * 4u;
+  // the emulated fold of dword w into chain register x
+  auto absorb = [&](uint32_t x, uint32_t w) {
+    x ^= w;
+    if constexpr (LK == 0) return x;
+    uint32_t y = 0;
+#pragma unroll
+    for (int q = 0; q < LK; ++q) y ^= *(const lds_u32*)(uintptr_t)(((x >> (8 * q)) & 0xFFu) * 128u + kc);
+    return y;
+  };
   // chunk t of lane: batch chunk lane + 64 t (clamped to the batch's last)
   auto chunk_off = [&](uint32_t b, int t) { return b * kBatch + 16u * min((uint32_t)(lane + 64 * t), kChunks - 1); };
   uint32_t in_ring = 0, rbase = b0;
@@ -68,12 +88,19 @@ __global__ void __launch_bounds__(64 * NW, 1) stage(const uint8_t* frames, uint3
     in_ring = 0;
   };
   // the "fold": lane f XORs its frame's 27 dwords from the slot
-  auto fold = [&](uint32_t slot, uint32_t r) {
-    uint32_t w = 0;
+  auto fold_regs = [&](const uint32_t* d) {
+    uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < (int)(S / 4); ++k) w ^= *(const lds_u32*)(uintptr_t)(slot + S * lane + 4u * k);
+    for (int k = 0; k < (int)(S / 4); ++k) c[k & 3] = absorb(c[k & 3], d[k]);
+    const uint32_t w = c[0] ^ c[1] ^ c[2] ^ c[3];
     *(lds_u32*)(uintptr_t)(kRing + 4u * (in_ring * NW * 64u + wave * 64u + lane)) = w;
     if (++in_ring == RING) flush();
+  };
+  auto fold = [&](uint32_t slot, uint32_t r) {
+    uint32_t d[S / 4];
+#pragma unroll
+    for (int k = 0; k < (int)(S / 4); ++k) d[k] = *(const lds_u32*)(uintptr_t)(slot + S * lane + 4u * k);
+    fold_regs(d);
   };
   if (nrounds == 0) return;  // (the whole workgroup: b0 >= b1 for every wave)
   if constexpr (MODE == 0) {
@@ -101,6 +128,29 @@ __global__ void __launch_bounds__(64 * NW, 1) stage(const uint8_t* frames, uint3
         __builtin_amdgcn_s_waitcnt(0xC07F);
       }
     }
+  } else if constexpr (MODE == 2) {
+    auto issue = [&](uint32_t b) {
+      b = min(b, b1 - 1);
+#pragma unroll
+      for (int t = 0; t < C; ++t)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(frames + chunk_off(b, t)),
+                                         (__attribute__((address_space(3))) void*)(uintptr_t)(slot0 + 1024u * t), 16, 0,
+                                         0);
+    };
+    issue(b0 + wave);
+    for (uint32_t r = 0; r < nrounds; ++r) {
+      WAIT_VM(0);  // batch r has landed in the slot
+      __asm__ __volatile__("" ::: "memory");
+      uint32_t d[S / 4];
+#pragma unroll
+      for (int k = 0; k < (int)(S / 4); ++k) d[k] = *(const lds_u32*)(uintptr_t)(slot0 + S * lane + 4u * k);
+      __asm__ __volatile__("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // the slot is read: refill it
+      __asm__ __volatile__("" ::: "memory");
+      issue(b0 + (r + 1) * NW + wave);
+      fold_regs(d);
+    }
+    WAIT_VM(0);
   } else {
     // batch chunk lane + 64 t lands at slot + 1024 t + 16 lane (the DMA's
     // per-lane LDS address); frame f's bytes therefore sit at slot + 108 f
@@ -167,10 +217,11 @@ int main() {
            rb / ts[15] / 1e6);
     fflush(stdout);
   };
-#define RUN(M, W, RG, NAME, DST)                                                                          \
+#define RUN(M, W, RG, NAME, DST) RUNL(M, W, RG, 0, NAME, DST)
+#define RUNL(M, W, RG, LK, NAME, DST)                                                                     \
   {                                                                                                       \
-    auto kf = stage<M, W, RG>;                                                                            \
-    const size_t lds = (size_t)W * (M == 0 ? 1 : 2) * kSlot + (size_t)RG * W * 256;                       \
+    auto kf = stage<M, W, RG, LK>;                                                                        \
+    const size_t lds = (LK ? 32768 : 0) + (size_t)W * (M == 1 ? 2 : 1) * kSlot + (size_t)RG * W * 256;    \
     if (lds <= 160 * 1024) {                                                                              \
       CK(hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
       run(NAME, [&] { hipLaunchKernelGGL(kf, dim3(ncu), dim3(64 * W), lds, 0, d, n, DST); });              \
@@ -184,6 +235,30 @@ int main() {
     CK(hipMemcpy(x.data(), ref, (size_t)n * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(y.data(), out, (size_t)n * 4, hipMemcpyDeviceToHost));
     printf("{\"words_equal\": %s}\n", x == y ? "true" : "false");
+  }
+  // round 4: DMA into one slot per wave, frames read to VGPRs before the refill
+  RUN(2, 12, 13, "lds-dma one slot 12w ring 13", out)
+  {
+    std::vector<uint32_t> x(n), y(n);
+    CK(hipMemcpy(x.data(), ref, (size_t)n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(y.data(), out, (size_t)n * 4, hipMemcpyDeviceToHost));
+    printf("{\"words_equal_mode2\": %s}\n", x == y ? "true" : "false");
+  }
+  RUNL(0, 12, 12, 4, "fold-emulated vgpr staging 12w ring 12", ref)
+  RUNL(2, 12, 12, 4, "fold-emulated lds-dma one slot 12w ring 12", out)
+  {
+    std::vector<uint32_t> x(n), y(n);
+    CK(hipMemcpy(x.data(), ref, (size_t)n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(y.data(), out, (size_t)n * 4, hipMemcpyDeviceToHost));
+    printf("{\"words_equal_fold\": %s}\n", x == y ? "true" : "false");
+  }
+  for (int rep = 0; rep < 2; ++rep) {
+    RUNL(0, 12, 12, 4, "fold-emulated vgpr staging 12w ring 12", out)
+    RUNL(2, 12, 12, 4, "fold-emulated lds-dma one slot 12w ring 12", out)
+    RUNL(2, 14, 5, 4, "fold-emulated lds-dma one slot 14w ring 5", out)
+    RUNL(2, 10, 20, 4, "fold-emulated lds-dma one slot 10w ring 20", out)
+    RUN(2, 12, 13, "lds-dma one slot 12w ring 13", out)
+    RUN(2, 16, 8, "lds-dma one slot 16w ring 8", out)
   }
   for (int rep = 0; rep < 2; ++rep) {
     RUN(0, 12, 13, "vgpr staging 12w ring 13", out)

@@ -19,7 +19,7 @@ step() {  # step <name> <seconds> <command...>: output in $O/<name>.log
 make -C oracle -s || exit 1
 step pytest_r04a 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
 step smoke_r04a 200 python -c "import __graft_entry__ as g; g.smoke()"
-step ragged_ab_r04a 600 python scripts/ragged_ab.py --rounds 2 scratch/libs/base.so scratch/libs/compact.so
+step ragged_ab_r04a 700 python scripts/ragged_ab.py --rounds 2 --cases u4,mix,cfg3 scratch/libs/base.so scratch/libs/compact_fast.so scratch/libs/compact_agg.so
 gcc -std=c99 -O2 -Iinclude scripts/latency_c.c -Lroce-sim_amd/roce_icrc -l:libroceicrc.so \
   -Wl,-rpath,$PWD/roce-sim_amd/roce_icrc -o $O/latency_c || exit 1
 step latency_c_r04a 300 ./$O/latency_c
