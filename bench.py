@@ -66,6 +66,11 @@ WORKLOADS = {
              "mixed-MTU {256..4096} RDMA_WRITE_MIDDLE frames packed back to back, ICRC verify "
              "(GPU fault injector hits ~3/1024 frames: ICRC and payload bit flips must fail, "
              "randomised masked fields must pass)"),
+    # the responder's dominant frame (src/roce_rq.py:767-776): device-resident
+    # ragged batches of ACKs, the compact tiny-batch phase of the ragged kernel
+    "ack": (4, 1 << 24, 0x1C2C0007,
+            "ACK frames (IPv4/UDP/BTH/AETH, 48 B) packed back to back, device-resident ragged "
+            "ICRC compute (offsets + lengths in HBM)"),
     # SURVEY 8(f) rows 1 + 3: frames built on the GPU from the MR, ICRC fused
     "seg": (4096, 1 << 20, 0x1C2C0006,
             "RC SEND of 256 KiB messages from a device MR, 4 KiB PMTU (FIRST + 62 MIDDLE + "
@@ -377,6 +382,60 @@ class RaggedVerify:
                 "pass": bool((ok == expect).all())}
 
 
+class RaggedCompute:
+    """ack: ACK-sized frames packed back to back, ragged descriptors in HBM,
+    ICRC compute (the responder's stream of acknowledgements)."""
+
+    mode = "compute"
+
+    def __init__(self, torch, eng, dev, payload, n, seed, rank, world):
+        from roce_icrc import synth
+        self.torch, self.eng, self.n = torch, eng, n
+        # opcode 0x11 (ACKNOWLEDGE): BTH + a 4-byte AETH, 48-B frames
+        self.buf, self.offs, self.lens = synth.mixed_mtu_frames(
+            n, mtus=(payload,), opcode=0x11, seed=seed if world == 1 else seed + rank)
+        self.covered = synth.covered_bytes(self.lens)
+        # C_i read + 4-B ICRC written + the 12-B descriptor (offset, length) read
+        self.alg_bytes = self.covered + 16 * n
+        self.d_frames = torch.from_numpy(self.buf).to(dev)
+        self.d_offs = torch.from_numpy(self.offs.view(np.int64)).to(dev)
+        self.d_lens = torch.from_numpy(self.lens.view(np.int32)).to(dev)
+        self.out = torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def step(self, sp):
+        self.eng.compute_batch_dev(self.d_frames, self.d_offs, self.d_lens, self.n, self.out,
+                                   stream=sp)
+
+    def upload(self, h_frames):
+        self.d_frames.copy_(h_frames, non_blocking=True)
+
+    def results(self):
+        return self.out.cpu().numpy().view(np.uint32).copy()
+
+    def lanes(self):
+        return "ragged default (compact tiny batches: one lane per frame)"
+
+    def check(self):
+        # as Strided.check: the last step's words written into the trailers
+        # all verify on the device, one frame with a payload bit flipped fails
+        torch, n = self.torch, self.n
+        trail = self.d_offs + self.d_lens.to(torch.int64) - 4
+        idx = (trail[:, None] + torch.arange(4, device=self.d_frames.device)[None, :]).reshape(-1)
+        saved = self.d_frames[idx].clone()
+        self.d_frames[idx] = self.out.view(torch.uint8).reshape(-1)
+        mid = n // 2
+        pos = int(self.offs[mid]) + int(self.lens[mid]) - 8  # the AETH dword (covered, unmasked)
+        self.d_frames[pos] ^= 1
+        ok = torch.zeros(n, dtype=torch.uint8, device=self.d_frames.device)
+        self.eng.verify_batch_dev(self.d_frames, self.d_offs, self.d_lens, n, ok)
+        okh = ok.cpu().numpy().astype(bool)
+        self.d_frames[pos] ^= 1
+        self.d_frames[idx] = saved
+        good = int(okh.sum())
+        return {"words_verified": good, "frames": n, "flipped_frame_fails": bool(not okh[mid]),
+                "pass": bool(good == n - 1 and not okh[mid])}
+
+
 SEG_MSG = 256 * 1024
 
 
@@ -677,7 +736,8 @@ def main():
     payload, n_default, seed, desc = WORKLOADS[args.workload]
     n = args.packets or n_default
     dev = torch.device("cuda", local)
-    W = {"cfg3": RaggedVerify, "seg": Segment, "cfg4": Shard}.get(args.workload, Strided)(
+    W = {"cfg3": RaggedVerify, "seg": Segment, "cfg4": Shard, "ack": RaggedCompute}.get(
+        args.workload, Strided)(
         torch, eng, dev, payload, n, seed, rank, world)
     n = W.n
     stream = torch.cuda.current_stream(dev)
