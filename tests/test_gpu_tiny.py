@@ -216,3 +216,23 @@ def test_compact_test_rejects_unsafe_layouts(engine):
     want2, _ = oracle_batch(buf2, offs2, lens2)
     got2, _ = _dev_compute(engine, buf2, offs2, lens2)
     np.testing.assert_array_equal(got2, want2)
+
+
+def test_bench_ack_workload_line():
+    """bench.py --workload ack (device-resident ragged ACK frames, the compact
+    tiny-batch phase): the line's device check and per-rank sampled parity
+    pass, with the ragged roofline accounting (frame + descriptor + word)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--workload", "ack", "--packets", "300000",
+           "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-e2e"]
+    r = subprocess.run(cmd, cwd=str(ROOT), capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["checks"]["pass"] and d["config"]["packets_per_gpu"] == 300000
+    assert all(m == 0 for m in d["parity"]["mismatches_per_rank"])
+    assert d["roofline"]["alg_bytes_per_launch"] == 300000 * (44 + 16)
