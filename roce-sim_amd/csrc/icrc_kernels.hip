@@ -1331,6 +1331,14 @@ constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
 #define RICRC_SMALL_TAIL_DIV 16
 #endif
 constexpr uint32_t kSmallTailDiv = RICRC_SMALL_TAIL_DIV;
+// Staging (A/B switch): 16-byte loads into registers issued two batches ahead,
+// written into the wave's slot with ds_write_b128 (default), or LDS-DMA
+// (global_load_lds_dwordx4) into the slot one batch ahead.
+#ifndef RICRC_SMALL_DMA
+#define RICRC_SMALL_DMA 0
+#endif
+constexpr bool kSmallDma = RICRC_SMALL_DMA != 0;
+constexpr uint32_t kSmallAhead = kSmallDma ? 1u : 2u;
 using SmallKeys = Keys8;
 // Mul(-32) for the combine: unreplicated in the last 4 KiB, or (SMALL_COMB8)
 // as 8 conflict-free copies in the high halves of the table rows, the output
@@ -1497,13 +1505,69 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       a.claims ? a.claims + (size_t)(a.epoch % kClaimSlots) * kMaxClaimBlocks : nullptr;
   if (claims && tid == 0) atomicExch(&claims[blockIdx.x], (unsigned long long)a.epoch << 32);
   uint32_t lim = bs_end > 0 ? bs_end - 1u : 0u;  // prefetch clamp (no clamp while claiming)
-  auto load = [&](uint32_t b, u32x4* Rg) {  // unconditional: clamped chunk index
+  auto load = [&](uint32_t b, u32x4* Rg) __attribute__((always_inline)) {  // unconditional: clamped chunk index
     const uint8_t* base = a.frames + (uint64_t)min(b, lim) * 64u * S;
+    if constexpr (kSmallDma) {
+      // LDS-DMA straight into the wave's slot: chunk lane + 64 t of the
+      // batch lands at stage + 1024 t + 16 lane, the register path's layout;
+      // lanes past the batch's last chunk stay idle (the slot holds exactly
+      // the batch)
 #pragma unroll
-    for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
+      for (int t = 0; t < C; ++t)
+        if ((uint32_t)(lane + 64 * t) < nchunk)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(base + 16u * (uint32_t)(lane + 64 * t)),
+              (__attribute__((address_space(3))) void*)(uintptr_t)(stage + 1024u * (uint32_t)t), 16, 0, 2);
+    } else {
+#pragma unroll
+      for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
+    }
+  };
+  // LDS-DMA staging (A/B switch): the slot's batch has landed; its frames are
+  // patched in LDS and read into registers, the slot is refilled with the
+  // next batch (in flight during the fold), the fold runs from registers
+  auto dma_fold = [&](uint32_t b, uint32_t bnext, bool live, bool to_ring) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch is in the slot
+    __asm__ __volatile__("" ::: "memory");
+    const uint32_t pb = stage + (uint32_t)lane * S;
+    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+    const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * n) : 0u;
+    int ihl;
+    uint32_t st = check(d0, d2, ihl);
+    uint32_t R;
+    if (__all((st & kPktFatal) == 0 && ihl == 5)) {
+      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+      __asm__ __volatile__("" ::: "memory");
+      const uint32_t pz = pb - 4u * (uint32_t)pad;
+      uint32_t D[4 * kSmallMaxSteps];
+#pragma unroll
+      for (int kp = 0; kp < 4 * kSmallMaxSteps; ++kp) D[kp] = kp < 4 * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
+      __asm__ __volatile__("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read
+      __asm__ __volatile__("" ::: "memory");
+      body_prio_hi();
+      load(bnext, nullptr);
+      body_prio_lo();
+      R = fold4([&](int, int kp) { return D[kp]; });
+    } else {
+      R = small_fold_masked<false, SmallKeys, kSmallComb>(nullptr, pb, ihl, n);
+      __asm__ __volatile__("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __asm__ __volatile__("" ::: "memory");
+      load(bnext, nullptr);
+    }
+    emit(b * 64u + (uint32_t)lane, live, st, R, trailer, kRing && to_ring);
+    __asm__ __volatile__("" ::: "memory");
   };
   auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext, bool live = true,
-                            bool to_ring = true) {  // (to the ring when there is one)
+                            bool to_ring = true) __attribute__((always_inline)) {  // (to the ring when there is one)
+    if constexpr (kSmallDma) {
+      dma_fold(b, bnext, live, to_ring);
+      return;
+    }
     // staging and the prefetch go out at raised wave priority: cfg5 +2.5 to
     // +12 % (4326 -> 4437-4855 GiB/s, 6 A/B rounds on two boxes; priority 1-2
     // +2-3 %; raising it for the output stores as well measured 12 % slower,
@@ -1547,7 +1611,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint32_t nrounds = (bs_end - b0 + nw - 1) / nw;
     u32x4 X[C], Y[C];
     load(b0 + (uint32_t)wave, X);
-    load(b0 + (uint32_t)wave + nw, Y);
+    if constexpr (!kSmallDma) load(b0 + (uint32_t)wave + nw, Y);
     ring_base = b0 * 64u;
     uint32_t in_ring = 0;
     auto flush = [&]() {
@@ -1572,11 +1636,11 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     };
     for (uint32_t r = 0; r < nrounds; r += 2) {
       uint32_t b = b0 + r * nw + (uint32_t)wave;
-      stage_and_fold(b, X, b + 2 * nw, b < bs_end);
+      stage_and_fold(b, X, b + kSmallAhead * nw, b < bs_end);
       if (++in_ring == rounds_cap) flush();
       if (r + 1 < nrounds) {
         b += nw;
-        stage_and_fold(b, Y, b + 2 * nw, b < bs_end);
+        stage_and_fold(b, Y, b + kSmallAhead * nw, b < bs_end);
         if (++in_ring == rounds_cap) flush();
       }
     }
@@ -1586,14 +1650,14 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const int cnt = first < bs_end ? (int)((bs_end - first + nw - 1) / nw) : 0;
     u32x4 X[C], Y[C];
     load(first, X);
-    load(first + nw, Y);
+    if constexpr (!kSmallDma) load(first + nw, Y);
     uint32_t b = first;
     int i = 0;
     for (; i + 1 < cnt; i += 2, b += 2 * nw) {
-      stage_and_fold(b, X, b + 2 * nw);
-      stage_and_fold(b + nw, Y, b + 3 * nw);
+      stage_and_fold(b, X, b + kSmallAhead * nw);
+      stage_and_fold(b + nw, Y, b + nw + kSmallAhead * nw);
     }
-    if (i < cnt) stage_and_fold(b, X, b + 2 * nw);
+    if (i < cnt) stage_and_fold(b, X, b + kSmallAhead * nw);
   }
   if (claims) {  // own tail, then up to kMaxVictims other workgroups' tails
     lim = 0xFFFFFFFFu;
@@ -1623,6 +1687,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       }
     }
   }
+  if constexpr (kSmallDma) __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA outlives its slot's use
   // the last batch, straight from global memory (one wave of the owning block)
   if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % nw) {
     const uint32_t pkt = last * 64u + (uint32_t)lane;
