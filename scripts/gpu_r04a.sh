@@ -33,4 +33,6 @@ step bench2_r04a 300 env ROCE_ICRC_BENCH_DEVICE=0 python bench.py --gpus 2 --pac
 step multi_r04a 300 python scripts/multi_host_rate.py
 step bench_cfg2_r04a 300 python bench.py --workload cfg2
 step bench_cfg5_r04a 300 python bench.py --workload cfg5
+# last: a probe that writes device memory from the host (a segfault ends the call)
+step pingpong_r04a 120 ./scratch/pingpong
 exit 0
