@@ -27,10 +27,12 @@ gcc -std=c99 -O2 -Iinclude scripts/latency_c.c -Lscratch/libs/polls4 -l:librocei
   -Wl,-rpath,$PWD/scratch/libs/polls4 -o $O/latency_c_polls4 || exit 1
 step latency_c_polls4_r04a 300 ./$O/latency_c_polls4
 step small_stage_r04a 120 ./scratch/small_stage
-step cfg5_ab_r04a 600 python scratch/bench_ab.py --workloads cfg5 --rounds 3 scratch/libs/compact.so scratch/libs/comb8.so scratch/libs/comb8w10.so
+step cfg5_ab_r04a 600 python scratch/bench_ab.py --workloads cfg5 --rounds 2 scratch/libs/base.so scratch/libs/small_dma.so scratch/libs/comb8.so scratch/libs/comb8w10.so
 step svc_r04a 300 python scripts/svc_contention.py
 step bench2_r04a 300 env ROCE_ICRC_BENCH_DEVICE=0 python bench.py --gpus 2 --packets 40000
 step multi_r04a 300 python scripts/multi_host_rate.py
 step bench_cfg2_r04a 300 python bench.py --workload cfg2
 step bench_cfg5_r04a 300 python bench.py --workload cfg5
+# last: a probe that writes device memory from the host (a segfault ends the call)
+step pingpong_r04a 120 ./scratch/pingpong
 exit 0
