@@ -260,6 +260,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   a.ok_out = ok;
   a.tables = c->d_tables;
   a.busy = device_busy(c->device);
+  a.frames_lo4 = (uint32_t)((uintptr_t)frames & 15u);
   HIP_TRY(hipSetDevice(c->device));
   if (!ragged && n > 0 && use_small(c, stride, len) && ((uintptr_t)frames & 3u) == 0) {
     if (c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
@@ -873,6 +874,9 @@ int batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames, size_t frames
     }
     shards_of[u].push_back(d);
   }
+  if (uniq.size() == 1)  // one context: the plain batch (its copies need no gather)
+    return host_ragged(uniq[0], frames, frames_bytes, offsets, lens, n, icrc_out, status_out,
+                       ok_out, verify);
   std::vector<int> rcs(nctx, RICRC_OK);
   auto run = [&](size_t u) {
     for (int d : shards_of[u]) {

@@ -31,6 +31,11 @@ struct IcrcArgs {
   uint32_t epoch;
   // the device's service busy word (host-mapped; nullable): see announce_batch
   uint64_t* busy;
+  // (uintptr_t)frames & 15, set by the launcher: the ragged kernel's compact
+  // test works on offsets from the 16-byte line below `frames` (an integer
+  // made from the pointer inside the kernel turned every frame load of the
+  // kernel into a flat load)
+  uint32_t frames_lo4;
 };
 
 // Claim counters: per stream (up to kClaimStreams streams per context; later

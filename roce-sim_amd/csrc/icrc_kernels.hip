@@ -860,6 +860,11 @@ constexpr bool kHistAgg = RICRC_HIST_AGG != 0;
 constexpr uint32_t kCompactSpan = 4096;                        // bytes one wave stages per batch
 constexpr int kCompactLoads = (int)(kCompactSpan / 16u / 64u);  // 16-byte loads per lane
 constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a batch may hold
+// batches a wave has in flight ahead of the one it folds (A/B switch)
+#ifndef RICRC_COMPACT_AHEAD
+#define RICRC_COMPACT_AHEAD 2
+#endif
+constexpr int kCompactAhead = RICRC_COMPACT_AHEAD;
 static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
               "every wave's staging slot inside the sort arrays");
 // the window's compact batches: {span start (u64), batch index, span bytes}
@@ -890,20 +895,16 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
   auto load = [&](int k, u32x4* X, uint32_t& L, uint64_t& O) {
     const Ent e = entry(k);
     const uint32_t last = (e.span + 15u) / 16u - 1u;
-    const uint8_t* base = (const uint8_t*)(uintptr_t)e.b16;
+    const uint8_t* base = a.frames + (e.b16 - a.frames_lo4);  // (b16: from the line below frames)
 #pragma unroll
     for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
     const uint32_t i = min(e.bi * 64u + (uint32_t)lane, (uint32_t)cnt - 1u);
     L = a.lens[w0 + i];
     O = a.offsets[w0 + i];
   };
-  int k = wave;
-  if (k >= ncb) return;
-  u32x4 X[kCompactLoads];
-  uint32_t Ln;
-  uint64_t On;
-  load(k, X, Ln, On);
-  for (; k < ncb; k += kIcrcWaves) {
+  // one listed batch: its chunks (in X) into the slot, X refilled with the
+  // batch two rounds ahead, then the fold
+  auto batch = [&](int k, u32x4* X, uint32_t& Ln, uint64_t& On) __attribute__((always_inline)) {
     const Ent e = entry(k);
     const uint32_t last = (e.span + 15u) / 16u - 1u;
     body_prio_hi();
@@ -913,11 +914,11 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
     __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
     const uint32_t L = Ln;
     const uint64_t O = On;
-    load(min(k + kIcrcWaves, ncb - 1), X, Ln, On);  // the next batch, in flight during the fold
+    load(min(k + kCompactAhead * kIcrcWaves, ncb - 1), X, Ln, On);  // in flight during the next fold(s)
     body_prio_lo();
     const uint32_t i = e.bi * 64u + (uint32_t)lane;
     const bool live = i < (uint32_t)cnt;
-    const uint32_t pb = slot + (uint32_t)((uint64_t)(uintptr_t)(a.frames + O) - e.b16);
+    const uint32_t pb = slot + (uint32_t)(a.frames_lo4 + O - e.b16);
     const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the descriptor pass checked every lane)
     const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
     const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
@@ -942,8 +943,11 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
       lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
       __asm__ __volatile__("" ::: "memory");
       int nsm = (n + 3) >> 2;
+      const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
+      if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+        for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+      }
       const int ns = __builtin_amdgcn_readfirstlane(nsm);
       const int pad = 4 * ns - n;
       const uint32_t pz = pb - 4u * (uint32_t)pad;
@@ -976,6 +980,26 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
       if (a.status_out) stg8<kPktStorePol>(a.status_out + w0 + i, st);
     }
     __asm__ __volatile__("" ::: "memory");
+  };
+  // batches wave, wave + W, ... (W = waves), kCompactAhead of them in flight
+  // ahead of the fold
+  int k = wave;
+  if (k >= ncb) return;
+  u32x4 X[kCompactLoads];
+  uint32_t Lx;
+  uint64_t Ox;
+  load(k, X, Lx, Ox);
+  if constexpr (kCompactAhead == 2) {
+    u32x4 Y[kCompactLoads];
+    uint32_t Ly;
+    uint64_t Oy;
+    load(min(k + kIcrcWaves, ncb - 1), Y, Ly, Oy);
+    for (; k < ncb; k += 2 * kIcrcWaves) {
+      batch(k, X, Lx, Ox);
+      if (k + kIcrcWaves < ncb) batch(k + kIcrcWaves, Y, Ly, Oy);
+    }
+  } else {
+    for (; k < ncb; k += kIcrcWaves) batch(k, X, Lx, Ox);
   }
 }
 
@@ -1059,9 +1083,52 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       Lr[r] = a.lens[w0 + ic];
       Or[r] = a.offsets[w0 + ic];
     }
-    // sort key, offset / 4 and length of window packet i (key -1: a compact
-    // batch's packet, left out of the sort)
-    auto describe_key = [&](int r, bool compact) {
+    uint32_t cbits = 0;  // (uniform) bit r: round r's batch is compact
+    // Phase 0's test, per descriptor round (wave-uniform: the wave's 64
+    // packets of the round): every live frame tiny, dword-aligned, after its
+    // left neighbour's end, and inside the 4 KiB from the first frame's
+    // 16-byte line.
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      bool compact = false;
+      // (uniform) lane 0 is live, and some frame of the round is tiny (a
+      // window without tiny frames pays one compare and one ballot per round)
+      if (r * kIcrcThreads + wave * 64 < cnt && __any(Lr[r] <= kCompactMaxLen)) {
+        const int nlive = min(64, cnt - (r * kIcrcThreads + wave * 64));  // (uniform)
+        const bool live = lane < nlive;
+        const uint32_t L = Lr[r];
+        const uint64_t addr = a.frames_lo4 + Or[r];  // (from the line below frames)
+        const uint64_t b16 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr >> 32))
+                               << 32)) & ~15ull;
+        // offsets inside the 4 KiB from b16 (a frame outside fails the test)
+        const uint64_t rel64 = addr - b16;
+        const uint32_t rel = rel64 < kCompactSpan ? (uint32_t)rel64 : 0xFFFF0000u;
+        const uint32_t end = rel + L;
+        // the left neighbour's end: one DPP wave shift (lane 0 gets 0)
+        const uint32_t prev_end =
+            (uint32_t)__builtin_amdgcn_update_dpp(0, (int)end, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+        const bool ok = !live || (L >= 44 && L <= kCompactMaxLen && (L & 3u) == 0 && (rel & 3u) == 0 &&
+                                  end <= kCompactSpan && rel >= prev_end);
+        compact = __all(ok);
+        if (compact) {
+          cbits |= 1u << r;
+          // in order without overlap: the last live frame ends the span
+          const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)end, nlive - 1);
+          if (lane == 0) {
+            const uint32_t slot = atomicAdd((uint32_t*)ncompact, 1u);
+            // (an opaque batch index: as a constant the compiler kept one
+            // 16-byte entry template per round live across the window loop)
+            uint32_t bid = (uint32_t)(r * kIcrcWaves + wave);
+            asm volatile("" : "+v"(bid));
+            *(lds_u32x4*)(uintptr_t)(kCompactList + 16u * slot) =
+                u32x4{(uint32_t)b16, (uint32_t)(b16 >> 32), bid, span};
+            atomicAdd((uint32_t*)ncompact_pkts, (uint32_t)nlive);
+          }
+        }
+      }
+      // sort key, offset / 4 and length of window packet i (key -1: a
+      // compact batch's packet, left out of the sort)
       const int i = tid + r * kIcrcThreads;
       int key = 0;
       offw[r] = kNoOff;
@@ -1078,48 +1145,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         }
       }
       keys[r] = compact ? -1 : key;
-      return i < cnt && !compact;
-    };
-    // Phase 0's test, per descriptor round (wave-uniform: the wave's 64
-    // packets of the round): every live frame tiny, dword-aligned, after its
-    // left neighbour's end, and inside the 4 KiB from the first frame's
-    // 16-byte line.
-#pragma unroll
-    for (int r = 0; r < KR; ++r) {
-      bool compact = false;
-      if (r * kIcrcThreads + wave * 64 < cnt) {  // (uniform) lane 0 is live
-        const bool live = tid + r * kIcrcThreads < cnt;
-        const uint32_t L = Lr[r];
-        const uint64_t addr = (uint64_t)(uintptr_t)(a.frames + Or[r]);
-        const uint64_t b16 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr) |
-                              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr >> 32))
-                               << 32)) & ~15ull;
-        const uint64_t end = addr + L;
-        const uint64_t prev_end =
-            (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)end, 1, 64) |
-            ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(end >> 32), 1, 64) << 32);
-        const bool ok = !live || (L >= 44 && L <= kCompactMaxLen && (L & 3u) == 0 && (addr & 3u) == 0 &&
-                                  addr >= b16 && end <= b16 + kCompactSpan &&
-                                  (lane == 0 || addr >= prev_end));
-        compact = __all(ok);
-        if (compact) {
-          uint32_t span = live ? (uint32_t)(end - b16) : 0u;
-#pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) span = max(span, (uint32_t)__shfl_xor((int)span, d, 64));
-          const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
-          if (lane == 0) {
-            const uint32_t slot = atomicAdd((uint32_t*)ncompact, 1u);
-            // (an opaque batch index: as a constant the compiler kept one
-            // 16-byte entry template per round live across the window loop)
-            uint32_t bid = (uint32_t)(r * kIcrcWaves + wave);
-            asm volatile("" : "+v"(bid));
-            *(lds_u32x4*)(uintptr_t)(kCompactList + 16u * slot) =
-                u32x4{(uint32_t)b16, (uint32_t)(b16 >> 32), bid, span};
-            atomicAdd((uint32_t*)ncompact_pkts, nlive);
-          }
-        }
-      }
-      const bool counted = describe_key(r, compact);
+      const bool counted = i < cnt && !compact;
       if constexpr (kHistAgg) {
         // one LDS atomic per distinct key of the wave (a wave of one key --
         // tiny frames, a homogeneous batch -- otherwise serialises 64 adds
@@ -1161,6 +1187,34 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
           for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
         }
         continue;
+      }
+      // the sort's descriptors again (L2 hits): recomputed rather than held
+      // in registers across phase 0, whose two batches in flight need them
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        const int ic = min(tid + r * kIcrcThreads, cnt - 1);
+        Lr[r] = a.lens[w0 + ic];
+        Or[r] = a.offsets[w0 + ic];
+      }
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        const bool compact = (cbits >> r) & 1u;
+        const int i = tid + r * kIcrcThreads;
+        int key = 0;
+        offw[r] = kNoOff;
+        lw[r] = 0;
+        if (i < cnt && !compact) {
+          const uint32_t L = Lr[r];
+          const uint64_t off = Or[r];
+          if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
+          lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
+          if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
+            const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
+            // bucket 0: tiny frames (and unusable ones, which cost nothing)
+            key = L <= kTinyLen ? 0 : min(NB - 1, 1 + (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
+          }
+        }
+        keys[r] = compact ? -1 : key;
       }
     }
     // (uniform) the window's tiny frames, sorted to its front
@@ -1874,6 +1928,15 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
   auto step = [&](const u32x4 head, const u32x4 bz) -> int {
     const uint64_t req = (uint64_t)head.x | ((uint64_t)head.y << 32);
     const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)req);
+    // a batch kernel started on the device less than busy_ticks ago: the
+    // wave answers what is pending and leaves (a caller that keeps the wave
+    // busy must not keep a batch workgroup off this CU: round 4 measured a
+    // batch 1.21x slower beside one thread calling back to back)
+    const uint64_t stamp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bz.x) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bz.y) << 32);
+    const bool batch_young =
+        stamp != 0 && (int64_t)(__builtin_amdgcn_s_memrealtime() - stamp) < (int64_t)s.busy_ticks;
+    const int served_rc = batch_young ? 2 : 1;
     if (seq != served) {
       const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before req
@@ -1916,7 +1979,7 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
         polls = 0;
         served = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
-        return 1;
+        return served_rc;
       }
       L &= ~kSvcInline;  // (a torn inline read: the frame at kSvcFrame, below)
       if (L & kSvcBurst) {
@@ -1986,7 +2049,7 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
         polls = 0;
         served = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
-        return 1;
+        return served_rc;
       }
       const Pkt p = describe<DPI>(frame, 0, true, 0, L <= kSvcMaxFrame ? L : 0u);
       Batch<kUnroll> b = issue_packet<LOG2G, false>(p, lane);
@@ -2009,14 +2072,11 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
       polls = 0;
       served = seq;
       t_last = __builtin_amdgcn_s_memrealtime();
-      return 1;
+      return served_rc;
     }
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)head.z) != 0u) return 2;  // stop
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    const uint64_t stamp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bz.x) |
-                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bz.y) << 32);
-    if (stamp != 0 && (int64_t)(now - stamp) < (int64_t)s.busy_ticks) return 2;  // a batch starts
-    if (now - t_last > s.idle_ticks) return 2;
+    if (batch_young) return 2;  // a batch starts
+    if (__builtin_amdgcn_s_memrealtime() - t_last > s.idle_ticks) return 2;
     __builtin_amdgcn_s_sleep(2);
     return 0;
   };

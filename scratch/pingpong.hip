@@ -57,6 +57,7 @@ static int run(const char* name, uint32_t* req_host_view, const uint32_t* req_de
   for (uint32_t i = 1; i <= n; ++i) {
     const auto t0 = std::chrono::steady_clock::now();
     __atomic_store_n(req_host_view, i, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();  // (device memory through the BAR is write-combined: flush)
     while (__atomic_load_n(ans, __ATOMIC_ACQUIRE) != i) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
         timed_out = true;
