@@ -1942,8 +1942,8 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the frame the host wrote before req
       uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(req >> 32));
       bool inl = false;
+      uint32_t d12[12];
       if (L & kSvcInline) {  // (uniform) the 48 bytes of lanes 1-3 against the check word
-        uint32_t d12[12];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           d12[4 * q + 0] = (uint32_t)__builtin_amdgcn_readlane((int)head.x, q + 1);
@@ -1955,9 +1955,55 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
               (L & ~kSvcInline) <= kSvcInlineMax;
       }
       if (inl) {
-        // the frame came with the poll (lanes 1-3 hold its 48 bytes): into LDS,
-        // then folded from there as a one-frame burst on this wave (G = 8)
         L &= ~kSvcInline;
+        const uint32_t d0 = d12[0], d2 = d12[2];
+        if ((L & 3u) == 0 && L >= 44 && ((d0 >> 4) & 0xFu) == 4u && (d0 & 0xFu) == 5u &&
+            ((d2 >> 8) & 0xFFu) == 17u) {
+          // IHL 5, IPv4/UDP, whole dwords (ACK, NAK, read request, atomic
+          // ack): lane p of the first 16 holds frame dword k = p - (16 - n)
+          // (zeros in front), masked; each lane multiplies its dword by
+          // x^(-32 p) (the bits of p: Mul(-32), Mul(-32)^2, Mul(-128),
+          // Mul(-256), the service's combine sets), the 16 lanes XOR, and
+          // Mul(-512) then Mul(1024) make it x^(32 (16 - p)) per dword: the
+          // register after the frame.  Five dependent table steps and a
+          // reduction instead of the group code's head, fold and combine.
+          const int n = (int)((L - 4u) >> 2);  // 10 or 11
+          const int p = lane & 15, k = p - (16 - n);
+          uint32_t v = 0;
+#pragma unroll
+          for (int j = 0; j < 12; ++j) v = k == j ? d12[j] : v;
+          v = fix_dword(v, k, 6, 8);
+          if (lane >= 16 || k < 0) v = 0;
+          constexpr uint32_t kC = SvcKeysL::kComb;  // Mul(-32), then Mul(-128 2^l)
+          uint32_t y = mul_comb(v, kC);
+          v = (p & 1) ? y : v;
+          y = mul_comb(mul_comb(v, kC), kC);
+          v = (p & 2) ? y : v;
+          y = mul_comb(v, kC + 4096u);
+          v = (p & 4) ? y : v;
+          y = mul_comb(v, kC + 2u * 4096u);
+          v = (p & 8) ? y : v;
+#pragma unroll
+          for (int d = 8; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d, 16);
+          v = mul_comb(v, kC + 3u * 4096u);  // Mul(-512)
+          uint32_t P = 0, T = 0;
+          SvcKeysS::make(lane).absorb(P, T, v);  // Mul(1024)
+          const uint32_t icrc = ~(P ^ T);
+          const uint32_t st = ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) ? kPktLenMismatch : 0u;
+          if (lane == 0) {
+            const uint64_t ans = (uint64_t)icrc | ((uint64_t)st << 32) | ((uint64_t)(seq & kSvcSeqMask) << 40);
+            r->t_seen = t_seen;
+            r->t_done = __builtin_amdgcn_s_memrealtime();
+            r->polls = polls;
+            __hip_atomic_store(&r->resp, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          polls = 0;
+          served = seq;
+          t_last = __builtin_amdgcn_s_memrealtime();
+          return served_rc;
+        }
+        // other inline frames: into LDS, then folded from there as a
+        // one-frame burst on this wave (G = 8)
         if (lane >= 1 && lane <= 3) *(lds_u32x4*)(uintptr_t)(kBurstStage + 16u * (uint32_t)(lane - 1)) = head;
         if (lane == 0)
           *(__attribute__((address_space(3))) uint64_t*)(uintptr_t)kSvcDescLds = (uint64_t)L << 32;
