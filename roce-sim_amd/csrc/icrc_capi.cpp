@@ -76,6 +76,9 @@ struct ricrc_ctx {
   };
   Stage ms[2];
   size_t ms_frames = 0;  // frame bytes each block holds
+  // the context's last batch launch on a device where a service has run
+  // (batch_launched / service_wait_batches)
+  hipEvent_t batch_ev = nullptr;
 };
 
 namespace {
@@ -237,6 +240,64 @@ unsigned long long* claim_region(ricrc_ctx* c, hipStream_t s, uint32_t* epoch) {
   return c->d_claims + r * (size_t)ricrc::kClaimSlots * ricrc::kMaxClaimBlocks;
 }
 
+// Batches in flight per device.  A resident service wave leaves when a batch
+// starts on its device (announce_batch), but a caller that relaunched it at
+// once put it back beside the running batch: relaunches during a batch cost
+// the batch far more than the CU the wave holds (round 4, svc_contention.py:
+// cfg2 kernel 1.37x with 1, 4 or 10 threads calling back to back and the wave
+// relaunched per call).  So every batch launch on a device where a service
+// has run records the launching context's event on its stream, and a wave is
+// relaunched only once every such event of the device has completed: per-packet
+// calls wait while a batch runs on the device, batches run undisturbed.
+std::mutex g_batch_mu;
+std::vector<ricrc_ctx*> g_batch_ctxs;  // contexts with a batch event
+
+void batch_launched(ricrc_ctx* c, hipStream_t s) {
+  if (!device_busy(c->device)) return;  // no service on the device (yet): nothing to hold back
+  if (!c->batch_ev) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    c->batch_ev = ev;
+    g_batch_ctxs.push_back(c);
+  }
+  (void)hipEventRecord(c->batch_ev, s);
+}
+
+void batch_forget(ricrc_ctx* c) {
+  if (!c->batch_ev) return;
+  {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    for (size_t i = 0; i < g_batch_ctxs.size(); ++i)
+      if (g_batch_ctxs[i] == c) {
+        g_batch_ctxs.erase(g_batch_ctxs.begin() + (long)i);
+        break;
+      }
+  }
+  (void)hipEventDestroy(c->batch_ev);
+  c->batch_ev = nullptr;
+}
+
+// Waits (at most kBatchWaitMax) until no batch launched through this library
+// is in flight on the context's device.
+constexpr auto kBatchWaitMax = std::chrono::milliseconds(200);
+void service_wait_batches(const ricrc_ctx* c) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    bool running = false;
+    {
+      std::lock_guard<std::mutex> lk(g_batch_mu);
+      for (const ricrc_ctx* x : g_batch_ctxs)
+        if (x->device == c->device && hipEventQuery(x->batch_ev) == hipErrorNotReady) {
+          running = true;
+          break;
+        }
+    }
+    if (!running || std::chrono::steady_clock::now() - t0 > kBatchWaitMax) return;
+    for (int i = 0; i < 256; ++i) __builtin_ia32_pause();
+  }
+}
+
 // The per-packet service's wave holds one CU's LDS while it runs: a context
 // about to launch batch work asks it to leave first (it does within a few
 // microseconds; the next ricrc_compute_one relaunches it).
@@ -269,6 +330,7 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
     if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
   }
+  batch_launched(c, s);
   return RICRC_OK;
 }
 
@@ -449,6 +511,7 @@ int seg_launch(ricrc_ctx* c, const uint8_t* d_mr, uint64_t mr_bytes, const ricrc
   service_pause(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(ricrc::launch_segment(a, seg_log2g(c, pmtu), c->num_cus, s));
+  batch_launched(c, s);
   return RICRC_OK;
 }
 
@@ -523,6 +586,7 @@ int service_ensure(ricrc_ctx* c) {
     }
   }
   c->svc_last = now;
+  service_wait_batches(c);  // (see batch_launched)
   HIP_TRY(hipStreamSynchronize(c->svc_stream));  // a leaving wave has left
   ricrc::ServiceRing* r = c->svc;
   __atomic_store_n(&r->stop, 0u, __ATOMIC_RELAXED);
@@ -960,6 +1024,7 @@ void ricrc_ctx_destroy(ricrc_ctx* c) {
   }
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  batch_forget(c);
   (void)hipFree(c->d_tables);
   (void)hipFree(c->d_claims);
   (void)hipFree(c->d_frames);

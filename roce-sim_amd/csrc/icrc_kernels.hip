@@ -860,9 +860,11 @@ constexpr bool kHistAgg = RICRC_HIST_AGG != 0;
 constexpr uint32_t kCompactSpan = 4096;                        // bytes one wave stages per batch
 constexpr int kCompactLoads = (int)(kCompactSpan / 16u / 64u);  // 16-byte loads per lane
 constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a batch may hold
-// batches a wave has in flight ahead of the one it folds (A/B switch)
+// batches a wave has in flight ahead of the one it folds (A/B switch; 2 A/B
+// rounds, profiles/r04c/ragged_ab_r04c.log, 2^24 ACK frames compute / verify:
+// one ahead 2062-2087 / 2088-2102 GiB/s, two ahead 1729-1758 / 1947-1970)
 #ifndef RICRC_COMPACT_AHEAD
-#define RICRC_COMPACT_AHEAD 2
+#define RICRC_COMPACT_AHEAD 1
 #endif
 constexpr int kCompactAhead = RICRC_COMPACT_AHEAD;
 static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
@@ -1385,11 +1387,13 @@ constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
 #define RICRC_SMALL_TAIL_DIV 16
 #endif
 constexpr uint32_t kSmallTailDiv = RICRC_SMALL_TAIL_DIV;
-// Staging (A/B switch): 16-byte loads into registers issued two batches ahead,
-// written into the wave's slot with ds_write_b128 (default), or LDS-DMA
-// (global_load_lds_dwordx4) into the slot one batch ahead.
+// Staging (A/B switch): LDS-DMA (global_load_lds_dwordx4) into the wave's slot
+// one batch ahead (default), or 16-byte loads into registers issued two
+// batches ahead and written into the slot with ds_write_b128.  cfg5 kernel ms,
+// 5 A/B rounds over two sessions (profiles/r04a, r04c cfg5_ab): register
+// staging 0.3102-0.3129, LDS-DMA 0.3058-0.3098 (-1.2 %).
 #ifndef RICRC_SMALL_DMA
-#define RICRC_SMALL_DMA 0
+#define RICRC_SMALL_DMA 1
 #endif
 constexpr bool kSmallDma = RICRC_SMALL_DMA != 0;
 constexpr uint32_t kSmallAhead = kSmallDma ? 1u : 2u;
