@@ -879,7 +879,10 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
                                                 int wave, int lane, uint32_t ok_lds) {
   const MixedKeysS kk = MixedKeysS::make(lane);  // Mul(128) is staged in the G = 4 half
   constexpr uint32_t kComb = MixedKeysS::kComb;   // Mul(-32)
-  const uint32_t slot = MixedLds::kPerm + (uint32_t)wave * kCompactSpan;
+  // (scalar: a per-lane copy was spilled, and its reload inside the batch
+  // loop waited for the next batch's loads too -- scratch shares vmcnt)
+  const uint32_t slot =
+      MixedLds::kPerm + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * kCompactSpan;
   struct Ent {
     uint64_t b16;
     uint32_t bi, span;
@@ -898,11 +901,12 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
     const Ent e = entry(k);
     const uint32_t last = (e.span + 15u) / 16u - 1u;
     const uint8_t* base = a.frames + (e.b16 - a.frames_lo4);  // (b16: from the line below frames)
-#pragma unroll
-    for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
+    // the descriptors first: waiting for them leaves the span loads in flight
     const uint32_t i = min(e.bi * 64u + (uint32_t)lane, (uint32_t)cnt - 1u);
     L = a.lens[w0 + i];
     O = a.offsets[w0 + i];
+#pragma unroll
+    for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
   };
   // one listed batch: its chunks (in X) into the slot, X refilled with the
   // batch two rounds ahead, then the fold

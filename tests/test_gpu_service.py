@@ -95,20 +95,23 @@ def test_service_paused_by_batch_work_on_the_same_context(engine):
         out.zero_()
 
 
-def test_batch_beside_ten_threads_of_per_packet_calls_is_not_slowed():
-    """A batch launch on one context while 10 other threads (the reference's
-    gRPC pool, src/sanity_side.py:383) call ricrc_icrc back to back, each with
-    its own resident service wave: every batch workgroup stamps the device's
-    busy word and those waves leave, so the batch is not held up by the CUs
-    they occupy (loose bound here; profiles/ holds the measured numbers)."""
+def test_batch_beside_per_packet_calls_of_other_threads_is_not_slowed():
+    """Batch launches on one context while 1 or 10 other threads (the
+    reference's gRPC pool, src/sanity_side.py:383) call ricrc_icrc back to
+    back, each with its own resident service wave: every batch workgroup
+    stamps the device's busy word, those waves leave, and no caller relaunches
+    its wave until the device's batches have completed (batch_launched /
+    service_wait_batches).  Round 4 measured 1.018 / 1.001 / 0.985 at K = 1 /
+    4 / 10 (profiles/r04d/svc_r04d.log; 1.37x before the relaunch gate); the
+    bound here leaves room for a shared box's noise."""
     sys.path.insert(0, str(ROOT / "scripts"))
     import svc_contention
-    r = svc_contention.run(packets=1 << 16, reps=30, ks=(0, 10))
-    k0, k10 = r["per_k"]["0"], r["per_k"]["10"]
-    assert k0["batch_bit_exact"] and k10["batch_bit_exact"]
-    assert not k10["errors"], k10["errors"]
-    assert k10["icrc_calls_during_batches"] > 0
-    assert k10["slowdown"] < 1.25, r
+    r = svc_contention.run(packets=1 << 18, reps=30, ks=(0, 1, 10))
+    for k in ("0", "1", "10"):
+        assert r["per_k"][k]["batch_bit_exact"], r
+        assert not r["per_k"][k]["errors"], r
+    assert r["per_k"]["1"]["slowdown"] < 1.08, r
+    assert r["per_k"]["10"]["slowdown"] < 1.08, r
 
 
 def test_wave_relaunched_for_a_pending_request_answers_it_at_once(engine):
