@@ -1063,11 +1063,35 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   lds_u32* ncompact = (lds_u32*)(uintptr_t)(LD::kBase - 12u);  // phase 0: batches listed
   lds_u32* ncompact_pkts = (lds_u32*)(uintptr_t)(LD::kBase - 16u);  // ... and their packets
   const bool from_back = ((tid >> 6) & 1) != 0;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (scalar: its per-lane copies were spilled)
   bool s_tiny = false;  // (uniform) the G = 4 half holds Mul(128) instead of Mul(512)
 
   const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
   const uint32_t wsz = p1 > p0 ? (p1 - p0 + nwin - 1) / nwin : 1;
+  constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
+  uint32_t Lr[KR];
+  uint64_t Or[KR];
+  // every descriptor load of the thread first (clamped, unconditional: a
+  // guarded load makes the compiler wait for each in turn)
+  auto load_descriptors = [&](uint32_t w, int n) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const int ic = min(tid + r * kIcrcThreads, n - 1);
+      Lr[r] = a.lens[w + ic];
+      Or[r] = a.offsets[w + ic];
+    }
+  };
+  // Lr / Or are dead once the keys are computed: their registers hold no
+  // value (freeze(poison)) from there to the next load, so the prefetch's
+  // path into the next iteration does not keep them live across the phases
+  auto kill_descriptors = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      Lr[r] = __builtin_nondeterministic_value(Lr[r]);
+      Or[r] = __builtin_nondeterministic_value(Or[r]);
+    }
+  };
+  bool pre = false;  // (uniform) Lr / Or already hold this window's descriptors
   for (uint32_t w0 = p0; w0 < p1; w0 += wsz) {
     const int cnt = (int)min(wsz, p1 - w0);
     if (tid < NB) hist[tid] = 0;
@@ -1076,19 +1100,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     if (tid == NB + 2) *ncompact = 0;
     if (tid == NB + 3) *ncompact_pkts = 0;
     __syncthreads();
-    constexpr int KR = (W + kIcrcThreads - 1) / kIcrcThreads;
     int keys[KR];
     uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
-    // every descriptor load of the thread first (clamped, unconditional: a
-    // guarded load makes the compiler wait for each in turn), then the keys
-    uint32_t Lr[KR];
-    uint64_t Or[KR];
-#pragma unroll
-    for (int r = 0; r < KR; ++r) {
-      const int ic = min(tid + r * kIcrcThreads, cnt - 1);
-      Lr[r] = a.lens[w0 + ic];
-      Or[r] = a.offsets[w0 + ic];
-    }
+    if (!pre) load_descriptors(w0, cnt);
+    pre = false;
     uint32_t cbits = 0;  // (uniform) bit r: round r's batch is compact
     // Phase 0's test, per descriptor round (wave-uniform: the wave's 64
     // packets of the round): every live frame tiny, dword-aligned, after its
@@ -1168,6 +1183,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         atomicAdd((uint32_t*)&hist[keys[r]], 1u);
       }
     }
+    kill_descriptors();
     __syncthreads();
     OutBuf ob = {0, 0};
     if constexpr (VERIFY) {
@@ -1185,6 +1201,13 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         s_tiny = true;
         __syncthreads();
       }
+      // a window of compact batches only (cs == 0) needs no descriptor after
+      // this point: the next window's go out now, in flight during phase 0
+      // (compute only: beside verify's phase 0 they spilled)
+      if (!VERIFY && cs == 0 && w0 + wsz < p1) {
+        load_descriptors(w0 + wsz, (int)min(wsz, p1 - (w0 + wsz)));
+        pre = true;
+      }
       compact_batches<VERIFY>(a, w0, cnt, ncb, wave, lane, LD::kOk);
       __syncthreads();  // the staging slots are the sort arrays again
       if (cs == 0) {  // (uniform) a window of compact batches only: nothing to sort
@@ -1195,13 +1218,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         continue;
       }
       // the sort's descriptors again (L2 hits): recomputed rather than held
-      // in registers across phase 0, whose two batches in flight need them
-#pragma unroll
-      for (int r = 0; r < KR; ++r) {
-        const int ic = min(tid + r * kIcrcThreads, cnt - 1);
-        Lr[r] = a.lens[w0 + ic];
-        Or[r] = a.offsets[w0 + ic];
-      }
+      // in registers across phase 0, whose batches in flight need them
+      load_descriptors(w0, cnt);
 #pragma unroll
       for (int r = 0; r < KR; ++r) {
         const bool compact = (cbits >> r) & 1u;
@@ -1222,6 +1240,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         }
         keys[r] = compact ? -1 : key;
       }
+      kill_descriptors();
     }
     // (uniform) the window's tiny frames, sorted to its front
     const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
