@@ -874,7 +874,7 @@ constexpr uint32_t kCompactList = MixedLds::kBytes;
 constexpr uint32_t kMixedLdsBytes = kCompactList + 16u * (uint32_t)(MixedLds::kWindow / 64);
 static_assert(kMixedLdsBytes <= 163840u, "LDS");
 
-template <bool VERIFY>
+template <bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, int cnt, int ncb,
                                                 int wave, int lane, uint32_t ok_lds) {
   const MixedKeysS kk = MixedKeysS::make(lane);  // Mul(128) is staged in the G = 4 half
@@ -897,8 +897,8 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
     return e;
   };
   // a batch's span chunks and its lanes' descriptors (unconditional, clamped)
-  auto load = [&](int k, u32x4* X, uint32_t& L, uint64_t& O) {
-    const Ent e = entry(k);
+  auto load = [&](int k, u32x4* X, uint32_t& L, uint64_t& O, Ent& e) {
+    e = entry(k);
     const uint32_t last = (e.span + 15u) / 16u - 1u;
     const uint8_t* base = a.frames + (e.b16 - a.frames_lo4);  // (b16: from the line below frames)
     // the descriptors first: waiting for them leaves the span loads in flight
@@ -909,9 +909,9 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
     for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
   };
   // one listed batch: its chunks (in X) into the slot, X refilled with the
-  // batch two rounds ahead, then the fold
-  auto batch = [&](int k, u32x4* X, uint32_t& Ln, uint64_t& On) __attribute__((always_inline)) {
-    const Ent e = entry(k);
+  // batch kCompactAhead rounds ahead, then the fold
+  auto batch = [&](int k, u32x4* X, uint32_t& Ln, uint64_t& On, Ent& En) __attribute__((always_inline)) {
+    const Ent e = En;
     const uint32_t last = (e.span + 15u) / 16u - 1u;
     body_prio_hi();
 #pragma unroll
@@ -920,7 +920,7 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
     __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
     const uint32_t L = Ln;
     const uint64_t O = On;
-    load(min(k + kCompactAhead * kIcrcWaves, ncb - 1), X, Ln, On);  // in flight during the next fold(s)
+    load(min(k + kCompactAhead * kIcrcWaves, ncb - 1), X, Ln, On, En);  // in flight during the next fold(s)
     body_prio_lo();
     const uint32_t i = e.bi * 64u + (uint32_t)lane;
     const bool live = i < (uint32_t)cnt;
@@ -982,8 +982,11 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
         if (good && !ok) st |= kPktIcrcMismatch;
         lds_wr8(ok_lds + i, ok ? 1u : 0u);
       }
-      if (a.icrc_out) stg32<kPktStorePol>(a.icrc_out + w0 + i, icrc);
-      if (a.status_out) stg8<kPktStorePol>(a.status_out + w0 + i, st);
+      // (OUTS is a template parameter: a store under a run-time test leaves
+      // the compiler a variable count of stores after the next batch's loads,
+      // and its wait for them then waits for the stores as well)
+      if constexpr ((OUTS & 1) != 0) stg32<kPktStorePol>(a.icrc_out + w0 + i, icrc);
+      if constexpr ((OUTS & 2) != 0) stg8<kPktStorePol>(a.status_out + w0 + i, st);
     }
     __asm__ __volatile__("" ::: "memory");
   };
@@ -994,18 +997,20 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
   u32x4 X[kCompactLoads];
   uint32_t Lx;
   uint64_t Ox;
-  load(k, X, Lx, Ox);
+  Ent Ex;
+  load(k, X, Lx, Ox, Ex);
   if constexpr (kCompactAhead == 2) {
     u32x4 Y[kCompactLoads];
     uint32_t Ly;
     uint64_t Oy;
-    load(min(k + kIcrcWaves, ncb - 1), Y, Ly, Oy);
+    Ent Ey;
+    load(min(k + kIcrcWaves, ncb - 1), Y, Ly, Oy, Ey);
     for (; k < ncb; k += 2 * kIcrcWaves) {
-      batch(k, X, Lx, Ox);
-      if (k + kIcrcWaves < ncb) batch(k + kIcrcWaves, Y, Ly, Oy);
+      batch(k, X, Lx, Ox, Ex);
+      if (k + kIcrcWaves < ncb) batch(k + kIcrcWaves, Y, Ly, Oy, Ey);
     }
   } else {
-    for (; k < ncb; k += kIcrcWaves) batch(k, X, Lx, Ox);
+    for (; k < ncb; k += kIcrcWaves) batch(k, X, Lx, Ox, Ex);
   }
 }
 
@@ -1208,7 +1213,14 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
         load_descriptors(w0 + wsz, (int)min(wsz, p1 - (w0 + wsz)));
         pre = true;
       }
-      compact_batches<VERIFY>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+      if (a.icrc_out && a.status_out)
+        compact_batches<VERIFY, 3>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+      else if (a.icrc_out)
+        compact_batches<VERIFY, 1>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+      else if (a.status_out)
+        compact_batches<VERIFY, 2>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+      else
+        compact_batches<VERIFY, 0>(a, w0, cnt, ncb, wave, lane, LD::kOk);
       __syncthreads();  // the staging slots are the sort arrays again
       if (cs == 0) {  // (uniform) a window of compact batches only: nothing to sort
         if constexpr (VERIFY) {

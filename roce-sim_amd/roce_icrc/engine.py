@@ -169,7 +169,10 @@ def load_library() -> ctypes.CDLL:
             f"{path} is not built; run `make -C roce-sim_amd` (or __graft_entry__.build())"
         )
     lib = ctypes.CDLL(str(path))
+    variant = bool(os.environ.get("ROCE_ICRC_LIB"))
     for name, (res, args) in _SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue  # (an A/B build older than this entry point: calling it raises)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
