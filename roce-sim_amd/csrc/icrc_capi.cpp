@@ -79,6 +79,8 @@ struct ricrc_ctx {
   // the context's last batch launch on a device where a service has run
   // (batch_launched / service_wait_batches)
   hipEvent_t batch_ev = nullptr;
+  // ragged launches: the host-mapped hint word (tiny_hint) of the context
+  uint32_t* tiny_hint = nullptr;
 };
 
 namespace {
@@ -305,6 +307,32 @@ void service_pause(ricrc_ctx* c) {
   if (c->svc_launched) __atomic_store_n(&c->svc->stop, 1u, __ATOMIC_RELEASE);
 }
 
+// Ragged kernel choice (icrc_ragged_mixed_kernel): each context owns one
+// word of a process-wide host-mapped block.  A ragged launch's first
+// workgroup stores into it whether its first 1024 packets hold a frame of at
+// most 128 bytes, and the context's later ragged launches run the kernel with
+// phase 0 while it is 1 (launches enqueued back to back all read what the
+// kernels finished before them wrote; a context's first ragged launch runs
+// without phase 0).  The words are never freed: a kernel launched on a
+// caller's stream may still write one after its context is destroyed (a
+// recycled word then only steers a choice, never a result).
+constexpr uint32_t kHintWords = 4096;
+std::mutex g_hint_mu;
+uint32_t* g_hints = nullptr;
+uint32_t g_hint_next = 0;
+
+uint32_t* hint_word() {
+  std::lock_guard<std::mutex> lk(g_hint_mu);
+  if (!g_hints) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, kHintWords * 64u, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return nullptr;  // (no hint: the kernel without phase 0, still exact)
+    std::memset(h, 0, kHintWords * 64u);
+    g_hints = (uint32_t*)h;
+  }
+  return g_hints + 16u * (g_hint_next++ % kHintWords);  // (one 64-byte line each)
+}
+
 int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint32_t* lens,
            uint64_t stride, uint32_t len, uint32_t n, uint32_t* icrc, uint8_t* status, uint8_t* ok,
            bool ragged, bool verify, int log2g, hipStream_t s) {
@@ -328,7 +356,15 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
     HIP_TRY(ricrc::launch_icrc_small(a, verify, c->num_cus, s));
   } else {
     if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
-    HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s));
+    bool compact = false;
+    if (ragged) {
+      if (!c->tiny_hint) c->tiny_hint = hint_word();
+      if (c->tiny_hint) {
+        compact = __atomic_load_n(c->tiny_hint, __ATOMIC_ACQUIRE) != 0u;
+        a.tiny_hint = c->tiny_hint;
+      }
+    }
+    HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s, compact));
   }
   batch_launched(c, s);
   return RICRC_OK;

@@ -36,6 +36,10 @@ struct IcrcArgs {
   // made from the pointer inside the kernel turned every frame load of the
   // kernel into a flat load)
   uint32_t frames_lo4;
+  // ragged mixed kernel: host-mapped word a workgroup sets when its first
+  // packets hold a frame of at most 128 bytes (nullable); the launcher picks
+  // the kernel with phase 0 for the context's next ragged launch from it
+  uint32_t* tiny_hint;
 };
 
 // Claim counters: per stream (up to kClaimStreams streams per context; later
@@ -50,7 +54,7 @@ void build_table_image(uint32_t* out);
 
 // Enqueues the ICRC kernel; returns a hipError_t.
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
-                       hipStream_t stream);
+                       hipStream_t stream, bool compact = false);
 
 // Strided frames of at most kSmallMaxStride bytes (stride a multiple of 4):
 // the lane-per-packet kernel with LDS-staged, coalesced loads.
@@ -66,6 +70,11 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink
 // device (icrc_capi.cpp, prepare_device).
 hipError_t prepare_kernels();
 hipError_t prepare_segment_kernels();
+// Raises a kernel's dynamic LDS limit and checks that it has no static LDS:
+// the kernels address LDS absolutely from 0 (tables, windows, slots), so a
+// static variable -- e.g. one a device-library reduction such as
+// __syncthreads_or brings in -- would sit under the tables.
+hipError_t set_dynamic_lds(const void* fn, int bytes);
 
 }  // namespace ricrc
 

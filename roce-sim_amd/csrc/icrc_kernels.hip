@@ -1041,18 +1041,15 @@ __device__ __forceinline__ void mixed_set(const IcrcArgs& a, int s, int e, uint3
   finish_packet<LOG2G, VERIFY, K, kMixedLut>(a, p, b, gl, grp * G, kk, ob);
 }
 
-template <bool VERIFY>
-__global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(IcrcArgs a) {
+// The workgroup's windows.  COMPACT: with the compact tiny batches (phase 0)
+// and their per-round test; without, the round-3 window loop.
+template <bool VERIFY, bool COMPACT>
+__device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
   constexpr int DPI = 32;  // sort key: G = 8 iterations
   using LD = MixedLds;
   constexpr int W = LD::kWindow;
   constexpr int NB = LD::kBuckets;
   static_assert(W + 16 < 65536, "claims are 16-bit counters");
-  const int tid = threadIdx.x;
-  announce_batch(a.busy);
-  stage_tables<3, kIcrcThreads, MixedKeysL>(a.tables, tid);
-  MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
-
   const int lane = tid & 63;
   const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
   const uint32_t p0 = blockIdx.x * per_block;
@@ -1079,6 +1076,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   // every descriptor load of the thread first (clamped, unconditional: a
   // guarded load makes the compiler wait for each in turn)
   auto load_descriptors = [&](uint32_t w, int n) __attribute__((always_inline)) {
+    // (an opaque window start: the compiler otherwise kept the addresses of
+    // the window's first loads for the reload after phase 0, 16 VGPR pairs
+    // live across it, and spilled them)
+    asm volatile("" : "+s"(w));
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const int ic = min(tid + r * kIcrcThreads, n - 1);
@@ -1102,8 +1103,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     if (tid < NB) hist[tid] = 0;
     if (tid == NB) *claim = 0;
     if (tid == NB + 1) *tclaim = 0;
-    if (tid == NB + 2) *ncompact = 0;
-    if (tid == NB + 3) *ncompact_pkts = 0;
+    if constexpr (COMPACT) {
+      if (tid == NB + 2) *ncompact = 0;
+      if (tid == NB + 3) *ncompact_pkts = 0;
+    }
     __syncthreads();
     int keys[KR];
     uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
@@ -1119,7 +1122,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       bool compact = false;
       // (uniform) lane 0 is live, and some frame of the round is tiny (a
       // window without tiny frames pays one compare and one ballot per round)
-      if (r * kIcrcThreads + wave * 64 < cnt && __any(Lr[r] <= kCompactMaxLen)) {
+      if (COMPACT && r * kIcrcThreads + wave * 64 < cnt && __any(Lr[r] <= kCompactMaxLen)) {
         const int nlive = min(64, cnt - (r * kIcrcThreads + wave * 64));  // (uniform)
         const bool live = lane < nlive;
         const uint32_t L = Lr[r];
@@ -1198,8 +1201,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
     }
     // ---- phase 0: the compact tiny batches, before the sort fills the arrays
     // their waves stage through; the rest of the window (cs packets) is sorted
+    int cs = cnt;  // (uniform) the packets the sort phases take
+    if constexpr (COMPACT) {
     const int ncb = (int)__builtin_amdgcn_readfirstlane((int)*ncompact);
-    const int cs = cnt - (int)__builtin_amdgcn_readfirstlane((int)*ncompact_pkts);
+    cs = cnt - (int)__builtin_amdgcn_readfirstlane((int)*ncompact_pkts);
     if (ncb > 0) {
       if (!s_tiny) {
         MixedKeysS::template stage<kIcrcThreads>(a.tables + 0 * 1024, tid);  // main set 0: Mul(128)
@@ -1254,6 +1259,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       }
       kill_descriptors();
     }
+    }  // COMPACT
     // (uniform) the window's tiny frames, sorted to its front
     const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
     const int ntiny = ntiny_all >= kTinyMin ? ntiny_all : 0;
@@ -1374,6 +1380,42 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
       for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
     }
   }
+}
+
+// Two kernels: with phase 0 (COMPACT) and without -- the round-3 window loop.
+// In one kernel, the phase-0 code cost cfg3 (no tiny frame) 1.5-3.5 %
+// (register allocation and layout, not work: profiles/r04i, r04j), and one
+// kernel holding both loops spilled the compact loop's descriptors (ACK
+// frames -7 %).  The launch's first workgroup probes its first kIcrcThreads
+// lengths while the tables are staged and stores into the context's hint word
+// whether one of them is at most kCompactMaxLen bytes (one store over PCIe per
+// launch: a store per wave made the ACK kernel 2.9x slower); the launcher
+// picks the kernel of the context's later ragged launches from it
+// (icrc_capi.cpp hint_word; both give the same words).
+template <bool VERIFY, bool COMPACT>
+__global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(IcrcArgs a) {
+  const int tid = threadIdx.x;
+  const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
+  const uint32_t p0 = blockIdx.x * per_block;
+  const uint32_t p1 = min(a.n, p0 + per_block);
+  const uint32_t probe = blockIdx.x == 0 && p0 < p1 ? a.lens[p0 + min((uint32_t)tid, p1 - p0 - 1u)] : 0xFFFFFFFFu;
+  announce_batch(a.busy);
+  stage_tables<3, kIcrcThreads, MixedKeysL>(a.tables, tid);
+  MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
+  if (a.tiny_hint && blockIdx.x == 0) {  // (uniform) one store over PCIe per launch
+    // the workgroup's OR through one word per wave in the compact list (free
+    // until the first window's test; __syncthreads_or would bring a static
+    // LDS variable, which would sit under the tables)
+    if ((tid & 63) == 0) lds_wr(kCompactList + 4u * (uint32_t)(tid >> 6), __any(probe <= kCompactMaxLen) ? 1u : 0u);
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t any = 0;
+#pragma unroll
+      for (int w = 0; w < kIcrcWaves; ++w) any |= lds_rd(kCompactList + 4u * (uint32_t)w);
+      __hip_atomic_store(a.tiny_hint, any ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  mixed_windows<VERIFY, COMPACT>(a, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -2218,22 +2260,24 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
 typedef void (*kernel_fn)(IcrcArgs);
 
 template <int LOG2G>
-kernel_fn pick(bool ragged, bool verify) {
-  if (ragged && LOG2G == 3 && RICRC_RAGGED_MIXED)
-    return verify ? icrc_ragged_mixed_kernel<true> : icrc_ragged_mixed_kernel<false>;
+kernel_fn pick(bool ragged, bool verify, bool compact) {
+  if (ragged && LOG2G == 3 && RICRC_RAGGED_MIXED) {
+    if (compact) return verify ? icrc_ragged_mixed_kernel<true, true> : icrc_ragged_mixed_kernel<false, true>;
+    return verify ? icrc_ragged_mixed_kernel<true, false> : icrc_ragged_mixed_kernel<false, false>;
+  }
   if (ragged) return verify ? icrc_ragged_kernel<LOG2G, true> : icrc_ragged_kernel<LOG2G, false>;
   return verify ? icrc_strided_kernel<LOG2G, true> : icrc_strided_kernel<LOG2G, false>;
 }
 
-kernel_fn select_kernel(int log2g, bool ragged, bool verify) {
+kernel_fn select_kernel(int log2g, bool ragged, bool verify, bool compact = false) {
   switch (log2g) {
-    case 0: return pick<0>(ragged, verify);
-    case 1: return pick<1>(ragged, verify);
-    case 2: return pick<2>(ragged, verify);
-    case 3: return pick<3>(ragged, verify);
-    case 4: return pick<4>(ragged, verify);
-    case 5: return pick<5>(ragged, verify);
-    case 6: return pick<6>(ragged, verify);
+    case 0: return pick<0>(ragged, verify, compact);
+    case 1: return pick<1>(ragged, verify, compact);
+    case 2: return pick<2>(ragged, verify, compact);
+    case 3: return pick<3>(ragged, verify, compact);
+    case 4: return pick<4>(ragged, verify, compact);
+    case 5: return pick<5>(ragged, verify, compact);
+    case 6: return pick<6>(ragged, verify, compact);
     default: return nullptr;
   }
 }
@@ -2276,24 +2320,29 @@ void build_table_image(uint32_t* out) {
   for (int l = 0; l < kMaxLog2G; ++l) table_set(-(128ll << l), comb + (1 + l) * 1024);
 }
 
+hipError_t set_dynamic_lds(const void* fn, int bytes) {
+  hipFuncAttributes fa;
+  hipError_t e = hipFuncGetAttributes(&fa, fn);
+  if (e != hipSuccess) return e;
+  if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 hipError_t prepare_kernels() {
   for (int l = 0; l <= kMaxLog2G; ++l)
     for (int r = 0; r < 2; ++r)
-      for (int v = 0; v < 2; ++v) {
-        hipError_t e = hipFuncSetAttribute((const void*)select_kernel(l, r, v),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_bytes(l, r));
-        if (e != hipSuccess) return e;
-      }
+      for (int v = 0; v < 2; ++v)
+        for (int c = 0; c < 2; ++c) {
+          hipError_t e = set_dynamic_lds((const void*)select_kernel(l, r, v, c), (int)lds_bytes(l, r));
+          if (e != hipSuccess) return e;
+        }
   for (int c : {4, 7, 8})
     for (int v = 0; v < 2; ++v)
       for (int o = 0; o < 4; ++o) {
-        hipError_t e = hipFuncSetAttribute((const void*)select_small(c, v, o),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        hipError_t e = set_dynamic_lds((const void*)select_small(c, v, o), 163840);
         if (e != hipSuccess) return e;
       }
-  hipError_t e = hipFuncSetAttribute((const void*)icrc_service_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSvcLds);
+  hipError_t e = set_dynamic_lds((const void*)icrc_service_kernel, (int)kSvcLds);
   if (e != hipSuccess) return e;
   return prepare_segment_kernels();
 }
@@ -2304,9 +2353,9 @@ hipError_t launch_service(const ServiceArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
-                       hipStream_t stream) {
+                       hipStream_t stream, bool compact) {
   if (a.n == 0) return hipSuccess;
-  kernel_fn k = select_kernel(log2g, ragged, verify);
+  kernel_fn k = select_kernel(log2g, ragged, verify, compact);
   if (!k) return hipErrorInvalidValue;
   const uint32_t ppw = 64u >> log2g;
   const uint64_t nsets = (a.n + ppw - 1) / ppw;

@@ -626,9 +626,7 @@ size_t seg_lds_bytes(int log2g) { return MainKeys::kComb + 4096u * (1 + log2g) +
 
 hipError_t prepare_segment_kernels() {
   for (int l = 1; l <= 4; ++l) {
-    hipError_t e = hipFuncSetAttribute((const void*)select_segment(l),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)seg_lds_bytes(l));
+    hipError_t e = set_dynamic_lds((const void*)select_segment(l), (int)seg_lds_bytes(l));
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -40,9 +40,17 @@ def _run(engine, buf, offs, lens, verify=False, flip_every=0):
     do = torch.from_numpy(offs.view(np.int64)).cuda()
     dl = torch.from_numpy(lens.view(np.int32)).cuda()
     out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    # every launch twice: the context's first look at tiny frames may run the
+    # ragged kernel without phase 0, the next runs the one with it (hint word,
+    # icrc_capi.cpp hint_word); both must give the same words
+    engine.compute_batch_dev(d, do, dl, n, out)
+    torch.cuda.synchronize()
+    first = out.cpu().numpy().view(np.uint32).copy()
+    out.zero_()
     engine.compute_batch_dev(d, do, dl, n, out)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32).copy()
+    np.testing.assert_array_equal(first, got)
     if not verify:
         return got, None
     # trailers from the GPU words, every flip_every-th frame corrupted
@@ -56,7 +64,13 @@ def _run(engine, buf, offs, lens, verify=False, flip_every=0):
     ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
     engine.verify_batch_dev(d, do, dl, n, ok)
     torch.cuda.synchronize()
-    return got, (ok.cpu().numpy().astype(bool), bad)
+    first_ok = ok.cpu().numpy().astype(bool)
+    ok.zero_()
+    engine.verify_batch_dev(d, do, dl, n, ok)
+    torch.cuda.synchronize()
+    ok_now = ok.cpu().numpy().astype(bool)
+    np.testing.assert_array_equal(first_ok, ok_now)
+    return got, (ok_now, bad)
 
 
 def test_ack_sized_batch_device_resident(engine):
@@ -236,3 +250,26 @@ def test_bench_ack_workload_line():
     assert d["checks"]["pass"] and d["config"]["packets_per_gpu"] == 300000
     assert all(m == 0 for m in d["parity"]["mismatches_per_rank"])
     assert d["roofline"]["alg_bytes_per_launch"] == 300000 * (44 + 16)
+
+
+def test_kernel_choice_follows_the_frames():
+    """A fresh context: its first ragged launch runs the kernel without phase 0
+    (no hint yet); after tiny frames the next runs the one with it, after a
+    batch without tiny frames the next runs without it again -- every word
+    bit-exact either way (cfg3-shaped frames, ACK frames, alternating)."""
+    torch = pytest.importorskip("torch")
+    from roce_icrc import IcrcEngine, synth
+    eng = IcrcEngine(0)
+    try:
+        cases = []
+        buf, offs, lens = synth.mixed_mtu_frames(20000, seed=7)
+        cases.append((buf, offs, lens))
+        buf, offs, lens = synth.mixed_mtu_frames(60000, mtus=(4,), opcode=0x11, seed=8)
+        cases.append((buf, offs, lens))
+        for buf, offs, lens in cases + cases + cases[::-1]:
+            want, _ = oracle_batch(buf, offs, lens)
+            got, _ = _run(eng, buf, offs, lens)
+            np.testing.assert_array_equal(got, want)
+    finally:
+        eng.close()
+
