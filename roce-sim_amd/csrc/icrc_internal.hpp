@@ -8,11 +8,13 @@
 namespace ricrc {
 
 // Device table image: 7 main sets (lanes-per-packet G = 1..64, log2 index) of
-// Mul(128 G), then the combine sets: [0] = Mul(-32), [1 + l] = Mul(-128 * 2^l).
+// Mul(128 G), then the combine sets: [0] = Mul(-32), [1 + l] = Mul(-128 * 2^l),
+// then Mul(64) (the small-frame kernel's two-chain fold).
 constexpr int kMaxLog2G = 6;
 constexpr int kNumMainSets = kMaxLog2G + 1;
 constexpr int kNumCombSets = kMaxLog2G + 1;
-constexpr int kTableWords = (kNumMainSets + kNumCombSets) * 1024;
+constexpr int kMul64Set = kNumMainSets + kNumCombSets;
+constexpr int kTableWords = (kMul64Set + 1) * 1024;
 
 struct IcrcArgs {
   const uint8_t* frames;

@@ -816,28 +816,32 @@ __device__ __forceinline__ uint32_t comb4(uint32_t x, const K& kk) {
   }
 }
 
-template <bool GLOBAL, class K, uint32_t COMB>
+template <bool GLOBAL, class K, uint32_t COMB, int CH = 4>
 __device__ __forceinline__ uint32_t fold_masked4(const uint8_t* f, uint32_t pb, int ihl, int n) {
+  // CH chains (K's table is Mul(32 CH)): chain c takes dwords k = CH j + c - pad
   const K kk = K::make(__lane_id());
-  const int ns = (n + 3) >> 2, pad = 4 * ns - n;
-  uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+  const int ns = (n + CH - 1) / CH, pad = CH * ns - n;
+  uint32_t P[CH], T[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) P[c] = T[c] = 0;
   for (int j = 0; j < ns; ++j) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = 4 * j + c - pad;
+    for (int c = 0; c < CH; ++c) {
+      const int k = CH * j + c - pad;
       uint32_t w = 0;
       if (k >= 0) w = fix_dword(GLOBAL ? ldg32(f + 4 * k) : lds_rd(pb + 4u * (uint32_t)k), k,
                                 ihl + 1, ihl + 3);
       kk.absorb(P[c], T[c], w);
     }
   }
-  uint32_t R = comb4<COMB>(P[3] ^ T[3], kk) ^ P[2] ^ T[2];
-  R = comb4<COMB>(R, kk) ^ P[1] ^ T[1];
-  return comb4<COMB>(R, kk) ^ P[0] ^ T[0];
+  uint32_t R = P[CH - 1] ^ T[CH - 1];
+#pragma unroll
+  for (int c = CH - 2; c >= 0; --c) R = comb4<COMB>(R, kk) ^ P[c] ^ T[c];
+  return R;
 }
-template <bool GLOBAL, class K, uint32_t COMB>
+template <bool GLOBAL, class K, uint32_t COMB, int CH = 4>
 __device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb, int ihl, int n) {
-  return fold_masked4<GLOBAL, K, COMB>(f, pb, ihl, n);
+  return fold_masked4<GLOBAL, K, COMB, CH>(f, pb, ihl, n);
 }
 
 // Window sort: wave-aggregated histogram / scatter atomics (A/B switch).
@@ -1498,7 +1502,18 @@ __device__ __forceinline__ uint32_t small_ring_quad(uint32_t tail, uint32_t i) {
   return i < kSmallHoleWords / 4u ? (i >> 3) * 256u + Keys8::kHole + (i & 7u) * 16u
                                   : tail + 16u * (i - kSmallHoleWords / 4u);
 }
-constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + 3) / 4;  // ns <= 8
+// Chains of the fold (A/B switch): two over Mul(64) (default), or four over
+// Mul(128).  Two need one Mul(-32) combine step instead of three and read one
+// pad dword at most: 108 lookups per 108-B frame instead of 124.  cfg5 kernel
+// ms, 6 A/B rounds over two sessions (profiles/r04p, r04q): four chains
+// 0.3050-0.3089, two 0.2980-0.3006 (-2.5 %), one (Mul(32), no combine, a
+// dependent chain of 26 lookups) 0.3257-0.3288.
+#ifndef RICRC_SMALL_CHAINS
+#define RICRC_SMALL_CHAINS 2
+#endif
+constexpr int kSmallChains = RICRC_SMALL_CHAINS;
+static_assert(kSmallChains == 2 || kSmallChains == 4, "chains");
+constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + kSmallChains - 1) / kSmallChains;
 #ifndef RICRC_SMALL_OUTBUF
 #define RICRC_SMALL_OUTBUF 64
 #endif
@@ -1524,9 +1539,10 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   announce_batch(a.busy);
   const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
   const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
-  const int ns = (n + 3) >> 2, pad = 4 * ns - n;  // steps, zero dwords in front
+  constexpr int CH = kSmallChains;
+  const int ns = (n + CH - 1) / CH, pad = CH * ns - n;  // steps, zero dwords in front
   {
-    const uint32_t* m128 = a.tables;  // main set 0: Mul(128)
+    const uint32_t* m128 = a.tables + (CH == 4 ? 0 : kMul64Set * 1024);  // Mul(32 CH)
     for (int i = tid; i < 2048; i += (int)blockDim.x) {  // 8 copies of 1024 words, 2 quads
       const int w = i >> 1, h = i & 1;  // w = t * 256 + e
       lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m128[w]);
@@ -1601,21 +1617,24 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   // (kp = k + pad, a compile-time index into the padded frame) ready to
   // absorb; dwords k < 0 are the zero pad
   auto fold4 = [&](auto rd) {
-    uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+    uint32_t P[CH], T[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) P[c] = T[c] = 0;
 #pragma unroll
     for (int j = 0; j < kSmallMaxSteps; ++j) {
       if (j < ns) {  // uniform
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int k = 4 * j + c - pad;
-          const uint32_t w = rd(k < 0 ? 0 : k, 4 * j + c);  // (never read before the frame)
+        for (int c = 0; c < CH; ++c) {
+          const int k = CH * j + c - pad;
+          const uint32_t w = rd(k < 0 ? 0 : k, CH * j + c);  // (never read before the frame)
           kk.absorb(P[c], T[c], (j == 0 && k < 0) ? 0u : w);
         }
       }
     }
-    uint32_t R = comb4<kSmallComb>(P[3] ^ T[3], kk) ^ P[2] ^ T[2];
-    R = comb4<kSmallComb>(R, kk) ^ P[1] ^ T[1];
-    return comb4<kSmallComb>(R, kk) ^ P[0] ^ T[0];
+    uint32_t R = P[CH - 1] ^ T[CH - 1];
+#pragma unroll
+    for (int c = CH - 2; c >= 0; --c) R = comb4<kSmallComb>(R, kk) ^ P[c] ^ T[c];
+    return R;
   };
   // per-dword masks (IPv4 options, the direct path, malformed frames)
 
@@ -1677,9 +1696,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
       __asm__ __volatile__("" ::: "memory");
       const uint32_t pz = pb - 4u * (uint32_t)pad;
-      uint32_t D[4 * kSmallMaxSteps];
+      uint32_t D[CH * kSmallMaxSteps];
 #pragma unroll
-      for (int kp = 0; kp < 4 * kSmallMaxSteps; ++kp) D[kp] = kp < 4 * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
+      for (int kp = 0; kp < CH * kSmallMaxSteps; ++kp) D[kp] = kp < CH * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
       __asm__ __volatile__("" ::: "memory");
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read
       __asm__ __volatile__("" ::: "memory");
@@ -1688,7 +1707,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       body_prio_lo();
       R = fold4([&](int, int kp) { return D[kp]; });
     } else {
-      R = small_fold_masked<false, SmallKeys, kSmallComb>(nullptr, pb, ihl, n);
+      R = small_fold_masked<false, SmallKeys, kSmallComb, CH>(nullptr, pb, ihl, n);
       __asm__ __volatile__("" ::: "memory");
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __asm__ __volatile__("" ::: "memory");
@@ -1729,7 +1748,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
       R = fold4([&](int, int kp) { return lds_rd(pz + 4u * (uint32_t)kp); });
     } else {
-      R = small_fold_masked<false, SmallKeys, kSmallComb>(nullptr, pb, ihl, n);
+      R = small_fold_masked<false, SmallKeys, kSmallComb, CH>(nullptr, pb, ihl, n);
     }
     emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing && to_ring);
     __asm__ __volatile__("" ::: "memory");
@@ -1830,7 +1849,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
     int ihl;
     const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
-    const uint32_t R = small_fold_masked<true, SmallKeys, kSmallComb>(f, 0u, ihl, n);
+    const uint32_t R = small_fold_masked<true, SmallKeys, kSmallComb, CH>(f, 0u, ihl, n);
     emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
   }
 }
@@ -2318,6 +2337,7 @@ void build_table_image(uint32_t* out) {
   uint32_t* comb = out + kNumMainSets * 1024;
   table_set(-32, comb);
   for (int l = 0; l < kMaxLog2G; ++l) table_set(-(128ll << l), comb + (1 + l) * 1024);
+  table_set(64, out + kMul64Set * 1024);
 }
 
 hipError_t set_dynamic_lds(const void* fn, int bytes) {
