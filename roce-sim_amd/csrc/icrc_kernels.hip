@@ -860,27 +860,28 @@ constexpr bool kHistAgg = RICRC_HIST_AGG != 0;
 // the small-frame kernel does (four Mul(128) chains, three Mul(-32) Horner
 // steps), and the next batch's span is in flight while this one folds.  The
 // descriptor pass finds the batches (one wave = 64 consecutive packets of one
-// descriptor round) and leaves them out of the sort.
+// descriptor round) and leaves them out of the sort; each wave folds the
+// compact batches of its OWN descriptor rounds, with the frame lengths and span
+// offsets that test left in its registers (round 4, session t: +6 % on ACK
+// frames against handing the batches round-robin to all waves, which had to
+// read every batch's descriptors a second time; profiles/r04t).
 constexpr uint32_t kCompactSpan = 4096;                        // bytes one wave stages per batch
 constexpr int kCompactLoads = (int)(kCompactSpan / 16u / 64u);  // 16-byte loads per lane
 constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a batch may hold
-// batches a wave has in flight ahead of the one it folds (A/B switch; 2 A/B
-// rounds, profiles/r04c/ragged_ab_r04c.log, 2^24 ACK frames compute / verify:
-// one ahead 2062-2087 / 2088-2102 GiB/s, two ahead 1729-1758 / 1947-1970)
-#ifndef RICRC_COMPACT_AHEAD
-#define RICRC_COMPACT_AHEAD 1
-#endif
-constexpr int kCompactAhead = RICRC_COMPACT_AHEAD;
 static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
               "every wave's staging slot inside the sort arrays");
-// the window's compact batches: {span start (u64), batch index, span bytes}
+// the window's compact batches, entry wave * KR + round: {span start (u64), -, span bytes}
 constexpr uint32_t kCompactList = MixedLds::kBytes;
 constexpr uint32_t kMixedLdsBytes = kCompactList + 16u * (uint32_t)(MixedLds::kWindow / 64);
 static_assert(kMixedLdsBytes <= 163840u, "LDS");
 
-template <bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
-__device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, int cnt, int ncb,
-                                                int wave, int lane, uint32_t ok_lds) {
+// Phase 0 of one wave: its compact rounds (bit r of cbits: the batch of packets
+// r * threads + wave * 64 + lane), Lr / relr = each lane's frame length and
+// its frame's offset in the round's span, from the descriptor pass.
+template <bool VERIFY, int OUTS, int KR>  // OUTS: 1 = icrc_out, 2 = status_out present
+__device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, int cnt, int wave, int lane,
+                                                uint32_t ok_lds, uint32_t cbits, const uint32_t (&Lr)[KR],
+                                                const uint32_t (&relr)[KR]) {
   const MixedKeysS kk = MixedKeysS::make(lane);  // Mul(128) is staged in the G = 4 half
   constexpr uint32_t kComb = MixedKeysS::kComb;   // Mul(-32)
   // (scalar: a per-lane copy was spilled, and its reload inside the batch
@@ -889,132 +890,117 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
       MixedLds::kPerm + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * kCompactSpan;
   struct Ent {
     uint64_t b16;
-    uint32_t bi, span;
+    uint32_t span;
   };
-  auto entry = [&](int k) {
-    const u32x4 v = *(const lds_u32x4*)(uintptr_t)(kCompactList + 16u * (uint32_t)k);
+  auto entry = [&](uint32_t r) {
+    const u32x4 v = *(const lds_u32x4*)(uintptr_t)(kCompactList + 16u * ((uint32_t)wave * KR + r));
     Ent e;
     e.b16 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.x) |
             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.y) << 32);
-    e.bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
     e.span = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
     return e;
   };
-  // a batch's span chunks and its lanes' descriptors (unconditional, clamped)
-  auto load = [&](int k, u32x4* X, uint32_t& L, uint64_t& O, Ent& e) {
-    e = entry(k);
+  // a batch's span chunks (unconditional, clamped)
+  auto issue = [&](const Ent& e, u32x4* X) __attribute__((always_inline)) {
     const uint32_t last = (e.span + 15u) / 16u - 1u;
     const uint8_t* base = a.frames + (e.b16 - a.frames_lo4);  // (b16: from the line below frames)
-    // the descriptors first: waiting for them leaves the span loads in flight
-    const uint32_t i = min(e.bi * 64u + (uint32_t)lane, (uint32_t)cnt - 1u);
-    L = a.lens[w0 + i];
-    O = a.offsets[w0 + i];
 #pragma unroll
     for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
   };
-  // one listed batch: its chunks (in X) into the slot, X refilled with the
-  // batch kCompactAhead rounds ahead, then the fold
-  auto batch = [&](int k, u32x4* X, uint32_t& Ln, uint64_t& On, Ent& En) __attribute__((always_inline)) {
-    const Ent e = En;
-    const uint32_t last = (e.span + 15u) / 16u - 1u;
-    body_prio_hi();
+  uint32_t todo = cbits;
+  if (todo == 0u) return;
+  u32x4 X[kCompactLoads];
+  Ent cur = entry((uint32_t)__builtin_ctz(todo));
+  issue(cur, X);
 #pragma unroll
-    for (int t = 0; t < kCompactLoads; ++t)
-      *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
-    __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
-    const uint32_t L = Ln;
-    const uint64_t O = On;
-    load(min(k + kCompactAhead * kIcrcWaves, ncb - 1), X, Ln, On, En);  // in flight during the next fold(s)
-    body_prio_lo();
-    const uint32_t i = e.bi * 64u + (uint32_t)lane;
-    const bool live = i < (uint32_t)cnt;
-    const uint32_t pb = slot + (uint32_t)(a.frames_lo4 + O - e.b16);
-    const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the descriptor pass checked every lane)
-    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
-    const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
-    uint32_t st = 0;
-    const int ihl = (int)(d0 & 0xFu);
-    if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
-      st |= kPktNotIpv4;
-    else if (((d2 >> 8) & 0xFFu) != 17u)
-      st |= kPktNotUdp;
-    else if (L < (uint32_t)(4 * ihl + 24))
-      st |= kPktBadLen;
-    if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
-    const bool good = (st & kPktFatal) == 0;
-    uint32_t R;
-    if (__all(good && ihl == 5)) {
-      // every frame IHL 5: masks and seed patched in place, then the four
-      // chains with the lane's own zero pad in front (absorbing zeros into a
-      // zero register keeps it zero, so shorter frames just start later)
-      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
-      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
-      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
-      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
-      __asm__ __volatile__("" ::: "memory");
-      int nsm = (n + 3) >> 2;
-      const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
-      if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
+  for (int r = 0; r < KR; ++r) {
+    if ((cbits >> r) & 1u) {  // (uniform)
+      const Ent e = cur;
+      const uint32_t last = (e.span + 15u) / 16u - 1u;
+      body_prio_hi();
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+      for (int t = 0; t < kCompactLoads; ++t)
+        *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
+      __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
+      todo &= ~(1u << r);
+      if (todo) {  // (uniform) the next compact round's span, in flight during this fold
+        cur = entry((uint32_t)__builtin_ctz(todo));
+        issue(cur, X);
       }
-      const int ns = __builtin_amdgcn_readfirstlane(nsm);
-      const int pad = 4 * ns - n;
-      const uint32_t pz = pb - 4u * (uint32_t)pad;
-      uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+      body_prio_lo();
+      const uint32_t L = Lr[r];
+      // (an opaque lane id per round: the compiler otherwise hoisted the
+      // output addresses of all rounds and spilled them)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const uint32_t i = (uint32_t)(r * kIcrcThreads + wave * 64 + ln);
+      const bool live = i < (uint32_t)cnt;
+      const uint32_t pb = slot + relr[r];
+      const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the descriptor pass checked every lane)
+      const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+      const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
+      uint32_t st = 0;
+      const int ihl = (int)(d0 & 0xFu);
+      if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
+        st |= kPktNotIpv4;
+      else if (((d2 >> 8) & 0xFFu) != 17u)
+        st |= kPktNotUdp;
+      else if (L < (uint32_t)(4 * ihl + 24))
+        st |= kPktBadLen;
+      if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
+      const bool good = (st & kPktFatal) == 0;
+      uint32_t R;
+      if (__all(good && ihl == 5)) {
+        // every frame IHL 5: masks and seed patched in place, then the four
+        // chains with the lane's own zero pad in front (absorbing zeros into a
+        // zero register keeps it zero, so shorter frames just start later)
+        lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+        lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+        lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+        lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+        __asm__ __volatile__("" ::: "memory");
+        int nsm = (n + 3) >> 2;
+        const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
+        if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
 #pragma unroll
-      for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
-        if (j < ns) {  // uniform
+          for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+        }
+        const int ns = __builtin_amdgcn_readfirstlane(nsm);
+        const int pad = 4 * ns - n;
+        const uint32_t pz = pb - 4u * (uint32_t)pad;
+        uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int kp = 4 * j + c;
-            const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
-            kk.absorb(P[c], T[c], kp >= pad ? w : 0u);
+        for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
+          if (j < ns) {  // uniform
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const int kp = 4 * j + c;
+              const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
+              kk.absorb(P[c], T[c], kp >= pad ? w : 0u);
+            }
           }
         }
+        R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
+        R = mul_comb(R, kComb) ^ P[1] ^ T[1];
+        R = mul_comb(R, kComb) ^ P[0] ^ T[0];
+      } else {
+        R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
       }
-      R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
-      R = mul_comb(R, kComb) ^ P[1] ^ T[1];
-      R = mul_comb(R, kComb) ^ P[0] ^ T[0];
-    } else {
-      R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
-    }
-    const uint32_t icrc = good ? ~R : 0u;
-    if (live) {
-      if constexpr (VERIFY) {
-        const bool ok = good && trailer == icrc;
-        if (good && !ok) st |= kPktIcrcMismatch;
-        lds_wr8(ok_lds + i, ok ? 1u : 0u);
+      const uint32_t icrc = good ? ~R : 0u;
+      if (live) {
+        if constexpr (VERIFY) {
+          const bool ok = good && trailer == icrc;
+          if (good && !ok) st |= kPktIcrcMismatch;
+          lds_wr8(ok_lds + i, ok ? 1u : 0u);
+        }
+        // (OUTS is a template parameter: a store under a run-time test leaves
+        // the compiler a variable count of stores after the next batch's loads,
+        // and its wait for them then waits for the stores as well)
+        if constexpr ((OUTS & 1) != 0) stg32<kPktStorePol>(a.icrc_out + w0 + i, icrc);
+        if constexpr ((OUTS & 2) != 0) stg8<kPktStorePol>(a.status_out + w0 + i, st);
       }
-      // (OUTS is a template parameter: a store under a run-time test leaves
-      // the compiler a variable count of stores after the next batch's loads,
-      // and its wait for them then waits for the stores as well)
-      if constexpr ((OUTS & 1) != 0) stg32<kPktStorePol>(a.icrc_out + w0 + i, icrc);
-      if constexpr ((OUTS & 2) != 0) stg8<kPktStorePol>(a.status_out + w0 + i, st);
+      __asm__ __volatile__("" ::: "memory");
     }
-    __asm__ __volatile__("" ::: "memory");
-  };
-  // batches wave, wave + W, ... (W = waves), kCompactAhead of them in flight
-  // ahead of the fold
-  int k = wave;
-  if (k >= ncb) return;
-  u32x4 X[kCompactLoads];
-  uint32_t Lx;
-  uint64_t Ox;
-  Ent Ex;
-  load(k, X, Lx, Ox, Ex);
-  if constexpr (kCompactAhead == 2) {
-    u32x4 Y[kCompactLoads];
-    uint32_t Ly;
-    uint64_t Oy;
-    Ent Ey;
-    load(min(k + kIcrcWaves, ncb - 1), Y, Ly, Oy, Ey);
-    for (; k < ncb; k += 2 * kIcrcWaves) {
-      batch(k, X, Lx, Ox, Ex);
-      if (k + kIcrcWaves < ncb) batch(k + kIcrcWaves, Y, Ly, Oy, Ey);
-    }
-  } else {
-    for (; k < ncb; k += kIcrcWaves) batch(k, X, Lx, Ox, Ex);
   }
 }
 
@@ -1092,8 +1078,8 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
     }
   };
   // Lr / Or are dead once the keys are computed: their registers hold no
-  // value (freeze(poison)) from there to the next load, so the prefetch's
-  // path into the next iteration does not keep them live across the phases
+  // value (freeze(poison)) from there to the next window's load, so the
+  // window loop's back edge does not keep them live across the phases
   auto kill_descriptors = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
@@ -1101,7 +1087,6 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
       Or[r] = __builtin_nondeterministic_value(Or[r]);
     }
   };
-  bool pre = false;  // (uniform) Lr / Or already hold this window's descriptors
   for (uint32_t w0 = p0; w0 < p1; w0 += wsz) {
     const int cnt = (int)min(wsz, p1 - w0);
     if (tid < NB) hist[tid] = 0;
@@ -1114,9 +1099,9 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
     __syncthreads();
     int keys[KR];
     uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
-    if (!pre) load_descriptors(w0, cnt);
-    pre = false;
+    load_descriptors(w0, cnt);
     uint32_t cbits = 0;  // (uniform) bit r: round r's batch is compact
+    uint32_t relr[KR];   // a compact round's frame offset in its span (phase 0)
     // Phase 0's test, per descriptor round (wave-uniform: the wave's 64
     // packets of the round): every live frame tiny, dword-aligned, after its
     // left neighbour's end, and inside the 4 KiB from the first frame's
@@ -1144,18 +1129,19 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
         const bool ok = !live || (L >= 44 && L <= kCompactMaxLen && (L & 3u) == 0 && (rel & 3u) == 0 &&
                                   end <= kCompactSpan && rel >= prev_end);
         compact = __all(ok);
+        relr[r] = rel;
         if (compact) {
           cbits |= 1u << r;
           // in order without overlap: the last live frame ends the span
           const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)end, nlive - 1);
           if (lane == 0) {
-            const uint32_t slot = atomicAdd((uint32_t*)ncompact, 1u);
-            // (an opaque batch index: as a constant the compiler kept one
+            atomicAdd((uint32_t*)ncompact, 1u);
+            // (an opaque third word: as a constant the compiler kept one
             // 16-byte entry template per round live across the window loop)
-            uint32_t bid = (uint32_t)(r * kIcrcWaves + wave);
-            asm volatile("" : "+v"(bid));
-            *(lds_u32x4*)(uintptr_t)(kCompactList + 16u * slot) =
-                u32x4{(uint32_t)b16, (uint32_t)(b16 >> 32), bid, span};
+            uint32_t z = 0;
+            asm volatile("" : "+v"(z));
+            *(lds_u32x4*)(uintptr_t)(kCompactList + 16u * (uint32_t)(wave * KR + r)) =
+                u32x4{(uint32_t)b16, (uint32_t)(b16 >> 32), z, span};
             atomicAdd((uint32_t*)ncompact_pkts, (uint32_t)nlive);
           }
         }
@@ -1195,7 +1181,12 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
         atomicAdd((uint32_t*)&hist[keys[r]], 1u);
       }
     }
-    kill_descriptors();
+    if constexpr (!COMPACT) {
+      kill_descriptors();
+    } else {
+#pragma unroll
+      for (int r = 0; r < KR; ++r) Or[r] = __builtin_nondeterministic_value(Or[r]);
+    }
     __syncthreads();
     OutBuf ob = {0, 0};
     if constexpr (VERIFY) {
@@ -1210,26 +1201,27 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
     const int ncb = (int)__builtin_amdgcn_readfirstlane((int)*ncompact);
     cs = cnt - (int)__builtin_amdgcn_readfirstlane((int)*ncompact_pkts);
     if (ncb > 0) {
+      // keys / offw / lw hold no value across phase 0 (recomputed after it)
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        keys[r] = __builtin_nondeterministic_value(keys[r]);
+        offw[r] = __builtin_nondeterministic_value(offw[r]);
+        lw[r] = __builtin_nondeterministic_value(lw[r]);
+      }
       if (!s_tiny) {
         MixedKeysS::template stage<kIcrcThreads>(a.tables + 0 * 1024, tid);  // main set 0: Mul(128)
         s_tiny = true;
         __syncthreads();
       }
-      // a window of compact batches only (cs == 0) needs no descriptor after
-      // this point: the next window's go out now, in flight during phase 0
-      // (compute only: beside verify's phase 0 they spilled)
-      if (!VERIFY && cs == 0 && w0 + wsz < p1) {
-        load_descriptors(w0 + wsz, (int)min(wsz, p1 - (w0 + wsz)));
-        pre = true;
-      }
+      // (Lr and relr are phase 0's lengths and span offsets; Or is dead)
       if (a.icrc_out && a.status_out)
-        compact_batches<VERIFY, 3>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+        compact_batches<VERIFY, 3, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
       else if (a.icrc_out)
-        compact_batches<VERIFY, 1>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+        compact_batches<VERIFY, 1, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
       else if (a.status_out)
-        compact_batches<VERIFY, 2>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+        compact_batches<VERIFY, 2, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
       else
-        compact_batches<VERIFY, 0>(a, w0, cnt, ncb, wave, lane, LD::kOk);
+        compact_batches<VERIFY, 0, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
       __syncthreads();  // the staging slots are the sort arrays again
       if (cs == 0) {  // (uniform) a window of compact batches only: nothing to sort
         if constexpr (VERIFY) {
@@ -1238,8 +1230,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
         }
         continue;
       }
-      // the sort's descriptors again (L2 hits): recomputed rather than held
-      // in registers across phase 0, whose batches in flight need them
+      // the sort's descriptors again (L2 hits) and its keys
       load_descriptors(w0, cnt);
 #pragma unroll
       for (int r = 0; r < KR; ++r) {
@@ -1261,8 +1252,10 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
         }
         keys[r] = compact ? -1 : key;
       }
-      kill_descriptors();
     }
+    kill_descriptors();  // (dead on every path from here to the next window's load)
+#pragma unroll
+    for (int r = 0; r < KR; ++r) relr[r] = __builtin_nondeterministic_value(relr[r]);
     }  // COMPACT
     // (uniform) the window's tiny frames, sorted to its front
     const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
