@@ -21,5 +21,5 @@ step() {  # step <name> <seconds> <command...>: output in $O/<name>.log
 step svc_$T 300 python scripts/svc_contention.py
 step multi_$T 300 python scripts/multi_host_rate.py --ks 1,2,8
 step latency_py_$T 300 python scripts/latency.py
-step sq_r04z 400 bash scripts/gpu_pmc_sq.sh $T ack cfg5
+step sq_$T 400 bash scripts/gpu_pmc_sq.sh $T ack cfg5
 exit 0
