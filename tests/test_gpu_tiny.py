@@ -232,6 +232,32 @@ def test_compact_test_rejects_unsafe_layouts(engine):
     np.testing.assert_array_equal(got2, want2)
 
 
+def test_compact_rounds_between_sorted_rounds(engine):
+    """Each wave folds the compact batches of its own descriptor rounds from
+    the lengths and span offsets of its test (icrc_kernels.hip,
+    compact_batches): 64-packet blocks that are all ACK-sized or all
+    longer frames, chosen per block, so a wave's compact and sorted rounds
+    interleave within a window; windows of compact rounds only; blocks
+    shifted by 32 packets (no round compact); a partial last window.
+    Compute and verify (flipped frames fail) against the oracle."""
+    rng = np.random.default_rng(31)
+    for n, shift, p_ack in ((8192 * 40 + 777, 0, 0.5), (8192 * 24 + 64 * 5, 0, 0.97),
+                            (8192 * 12 + 100, 32, 0.5)):
+        nb = (n + shift + 63) // 64
+        ack = rng.random(nb) < p_ack
+        blk = (np.arange(n) + shift) // 64
+        tiny = rng.choice([44, 48, 48, 48, 52, 64], n)  # (64 of them fit in 4 KiB)
+        big = rng.integers(33, 1100, n) * 4
+        lens = np.where(ack[blk], tiny, big).astype(np.uint32)
+        buf, offs, lens = _ragged(lens, n % 997)
+        want, _ = oracle_batch(buf, offs, lens)
+        got, (ok, bad) = _run(engine, buf, offs, lens, verify=True, flip_every=83)
+        np.testing.assert_array_equal(got, want, err_msg=f"n {n} shift {shift}")
+        expect = np.ones(n, bool)
+        expect[bad] = False
+        np.testing.assert_array_equal(ok, expect, err_msg=f"n {n} shift {shift}")
+
+
 def test_bench_ack_workload_line():
     """bench.py --workload ack (device-resident ragged ACK frames, the compact
     tiny-batch phase): the line's device check and per-rank sampled parity
