@@ -870,6 +870,13 @@ constexpr int kCompactLoads = (int)(kCompactSpan / 16u / 64u);  // 16-byte loads
 constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a batch may hold
 static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
               "every wave's staging slot inside the sort arrays");
+// a batch's words (one coalesced 256-B store per wave) are written
+// non-temporally: ACK bench +1.6-3 % over 3 A/B rounds against the default
+// policy (whole-library nt builds: cfg3 neutral; sc1 -1.5 %; profiles/r04x)
+#ifndef RICRC_COMPACT_STORE_POL
+#define RICRC_COMPACT_STORE_POL 2
+#endif
+constexpr int kCompactStorePol = RICRC_COMPACT_STORE_POL;
 // the window's compact batches, entry wave * KR + round: {span start (u64), -, span bytes}
 constexpr uint32_t kCompactList = MixedLds::kBytes;
 constexpr uint32_t kMixedLdsBytes = kCompactList + 16u * (uint32_t)(MixedLds::kWindow / 64);
@@ -996,8 +1003,8 @@ __device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, 
         // (OUTS is a template parameter: a store under a run-time test leaves
         // the compiler a variable count of stores after the next batch's loads,
         // and its wait for them then waits for the stores as well)
-        if constexpr ((OUTS & 1) != 0) stg32<kPktStorePol>(a.icrc_out + w0 + i, icrc);
-        if constexpr ((OUTS & 2) != 0) stg8<kPktStorePol>(a.status_out + w0 + i, st);
+        if constexpr ((OUTS & 1) != 0) stg32<kCompactStorePol>(a.icrc_out + w0 + i, icrc);
+        if constexpr ((OUTS & 2) != 0) stg8<kCompactStorePol>(a.status_out + w0 + i, st);
       }
       __asm__ __volatile__("" ::: "memory");
     }
