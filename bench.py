@@ -395,12 +395,19 @@ class RaggedCompute:
         self.buf, self.offs, self.lens = synth.mixed_mtu_frames(
             n, mtus=(payload,), opcode=0x11, seed=seed if world == 1 else seed + rank)
         self.covered = synth.covered_bytes(self.lens)
-        # C_i read + 4-B ICRC written + the 12-B descriptor (offset, length) read
-        self.alg_bytes = self.covered + 16 * n
+        # C_i read + 4-B ICRC written (48 B per ACK frame); the
+        # 12-B descriptors (offset, length) are excluded and reported separately
+        self.alg_bytes = self.covered + 4 * n
+        self.descriptor_bytes = 12 * n
         self.d_frames = torch.from_numpy(self.buf).to(dev)
         self.d_offs = torch.from_numpy(self.offs.view(np.int64)).to(dev)
         self.d_lens = torch.from_numpy(self.lens.view(np.int32)).to(dev)
         self.out = torch.zeros(n, dtype=torch.int32, device=dev)
+        # the responder knows its stream is ACKs: the ragged kernel with the
+        # compact tiny-batch phase on every launch (not the learned AUTO hint,
+        # which follows the last launch finished before each one)
+        from roce_icrc import engine as E
+        eng.set_ragged_variant(E.RAGGED_COMPACT)
 
     def step(self, sp):
         self.eng.compute_batch_dev(self.d_frames, self.d_offs, self.d_lens, self.n, self.out,
@@ -678,6 +685,34 @@ def enqueue_ceiling(torch, eng, W, stream, sp, dev):
     return result
 
 
+def gather_ranks(dist, world: int, rank: int, device: int, wall_s: float, kern_s, covered: int):
+    """Per-rank timing (per-GPU and aggregate rates):
+    every rank's own wall time of the K timed steps, kernel mean and covered
+    bytes, gathered (gloo) beside the MAX-reduce that gives `value`; rank
+    order."""
+    mine = {"rank": rank, "device": device, "wall_s": float(wall_s),
+            "kernel_ms": float(np.mean(kern_s)) * 1e3, "covered": int(covered)}
+    if world == 1:
+        return [mine]
+    ranks = [None] * world
+    dist.all_gather_object(ranks, mine)
+    return sorted(ranks, key=lambda r: r["rank"])
+
+
+def rank_fields(ranks, steps: int) -> dict:
+    """The line's per-rank keys: each rank's covered bytes of its K steps over
+    its own wall time (GiB/s), its kernel mean (ms) and the rate over that
+    mean, and the device it ran on.  (The slowest rank sets the aggregate: a
+    slow rank or XCD shows here, not in the MAX alone.)"""
+    return {
+        "per_rank_GiBps": [round(r["covered"] * steps / r["wall_s"] / 2**30, 3) for r in ranks],
+        "per_rank_kernel_ms": [round(r["kernel_ms"], 4) for r in ranks],
+        "per_rank_kernel_GiBps": [round(r["covered"] / (r["kernel_ms"] * 1e-3) / 2**30, 3)
+                                  for r in ranks],
+        "per_rank_device": [r["device"] for r in ranks],
+    }
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -775,6 +810,12 @@ def main():
     if world > 1:
         dist.barrier()
     kern_s = [a.elapsed_time(b) * 1e-3 for a, b in evs]
+    # the ragged kernel variant the timed launches ran (the last launch's: the
+    # variant is fixed per launch on the host, include/roce_icrc.h)
+    ragged_kernel = None
+    if isinstance(W, (RaggedVerify, RaggedCompute)):
+        ragged_kernel = {1: "compact (tiny-batch phase)", 2: "sorted"}.get(
+            eng.last_ragged_variant(), "none")
     ceil_key, ceil_gbps, ceil_ts = ceiling()
     if os.environ.get("ROCE_ICRC_BENCH_TRACE"):  # per-launch times (us) to stderr
         us = lambda xs: [round(x * 1e6) for x in xs]  # noqa: E731
@@ -787,6 +828,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t[0])
+    ranks = gather_ranks(dist, world, rank, local, t_local, kern_s, W.covered)
     gpu_icrc = W.results()
     checks = W.check()
     parity = parity_leg(W, gpu_icrc, seed + 101 * rank)
@@ -870,6 +912,7 @@ def main():
                 "packets_per_gpu": n,
                 "covered_bytes_per_gpu": W.covered,
                 "lanes_per_packet": args.lanes or W.lanes(),
+                **({"ragged_kernel": ragged_kernel} if ragged_kernel else {}),
                 "parallelism": f"{world} GPU(s), round-robin packet shards, no collective",
             },
             "roofline": {
@@ -881,6 +924,10 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": W.alg_bytes,
+                **({"descriptor_bytes_per_launch": W.descriptor_bytes,
+                    "frac_with_descriptors": round((W.alg_bytes + W.descriptor_bytes) / mean_k / 1e9
+                                                   / HBM_PEAK_GBPS, 4)}
+                   if hasattr(W, "descriptor_bytes") else {}),
             },
             "cpu_baseline": cpu,
             "parity": {
@@ -890,7 +937,9 @@ def main():
                 "what": parities[0]["what"],
                 "pass": all(p["mismatches"] == 0 for p in parities),
             },
+            # the aggregate / N, and every rank's own numbers (rank_fields)
             "per_gpu_GiBps": round(value / world, 3),
+            **rank_fields(ranks, args.steps),
             "kernel_ms_mean": round(mean_k * 1e3, 4),
             ceil_key: round(ceil_gbps, 1),
             "end_to_end_GiBps": None if e2e is None else round(e2e, 3),

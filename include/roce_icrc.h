@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define RICRC_ABI_VERSION 4
+#define RICRC_ABI_VERSION 5
 
 /* call-level return codes */
 #define RICRC_OK 0
@@ -94,6 +94,36 @@ void ricrc_ctx_destroy(ricrc_ctx* ctx);
 int ricrc_ctx_set_lanes_per_packet(ricrc_ctx* ctx, int lanes);
 /* The hipStream_t the synchronous host-buffer calls run on. */
 void* ricrc_ctx_stream(ricrc_ctx* ctx);
+
+/* Ragged-kernel variant (ABI 5).  The mixed-width ragged kernel (automatic
+ * lanes, or 8) comes in two builds: one with the compact tiny-batch phase,
+ * which folds packed runs of 64 frames of at most 128 bytes lane-per-packet
+ * without the window sort (a responder's ACK / NAK / atomic-ack stream,
+ * src/roce_rq.py:767-853), and one without it (every frame through the sort;
+ * mixed-MTU data, src/roce_v2.py:327-372).  Both give the same words; each is
+ * the faster one for its composition (ACK frames: compact ~1.5x; no tiny
+ * frames: sorted 1.5-3.5 %).
+ *   RICRC_RAGGED_AUTO     default.  Host-buffer calls decide per call from
+ *                         the lengths they hold (compact when at least 1/16
+ *                         of the batch's 64-frame groups are all tiny).
+ *                         Device-resident calls cannot see the lengths: they
+ *                         follow the context's learned hint, which the
+ *                         previous ragged launch's first workgroup sets from
+ *                         its first 1024 lengths -- so launches enqueued back
+ *                         to back follow the last launch FINISHED before them.
+ *   RICRC_RAGGED_COMPACT  every ragged launch of the context runs the kernel
+ *                         with the compact phase.
+ *   RICRC_RAGGED_SORTED   ... the kernel without it.
+ * A context is single-threaded, so a caller whose device-resident batches
+ * alternate composition sets the variant before each call. */
+#define RICRC_RAGGED_AUTO 0
+#define RICRC_RAGGED_COMPACT 1
+#define RICRC_RAGGED_SORTED 2
+int ricrc_ctx_set_ragged_variant(ricrc_ctx* ctx, int variant);
+/* The variant the context's last ragged launch ran (RICRC_RAGGED_COMPACT or
+ * RICRC_RAGGED_SORTED; RICRC_RAGGED_SORTED also for the single-width ragged
+ * kernels, which have no compact phase), RICRC_RAGGED_AUTO before any. */
+int ricrc_ctx_last_ragged_variant(ricrc_ctx* ctx, int* variant_out);
 
 /* ---- host buffers, synchronous (H2D + kernel + D2H) --------------------- */
 /* The per-packet drop-in for BTH.compute_icrc (src/roce.py:192): one wire

@@ -76,11 +76,18 @@ struct ricrc_ctx {
   };
   Stage ms[2];
   size_t ms_frames = 0;  // frame bytes each block holds
-  // the context's last batch launch on a device where a service has run
-  // (batch_launched / service_wait_batches)
-  hipEvent_t batch_ev = nullptr;
-  // ragged launches: the host-mapped hint word (tiny_hint) of the context
+  // the context's last batch launch per stream on a device where a service
+  // has run (batch_launched / service_wait_batches)
+  struct BatchEv {
+    hipStream_t stream;
+    hipEvent_t ev;
+  };
+  std::vector<BatchEv> batch_evs;
+  // ragged launches: the host-mapped hint word (tiny_hint) of the context, the
+  // caller's variant (RICRC_RAGGED_*) and the one the last launch ran
   uint32_t* tiny_hint = nullptr;
+  int ragged_variant = RICRC_RAGGED_AUTO;
+  int last_ragged = RICRC_RAGGED_AUTO;
 };
 
 namespace {
@@ -248,26 +255,36 @@ unsigned long long* claim_region(ricrc_ctx* c, hipStream_t s, uint32_t* epoch) {
 // the batch far more than the CU the wave holds (round 4, svc_contention.py:
 // cfg2 kernel 1.37x with 1, 4 or 10 threads calling back to back and the wave
 // relaunched per call).  So every batch launch on a device where a service
-// has run records the launching context's event on its stream, and a wave is
-// relaunched only once every such event of the device has completed: per-packet
-// calls wait while a batch runs on the device, batches run undisturbed.
+// has run records an event on its stream (one per context and stream: an
+// earlier batch of the same context on another caller stream stays tracked),
+// and a wave is relaunched only once every such event of the device has
+// completed: per-packet calls wait while a batch runs on the device, batches
+// run undisturbed.
 std::mutex g_batch_mu;
-std::vector<ricrc_ctx*> g_batch_ctxs;  // contexts with a batch event
+std::vector<ricrc_ctx*> g_batch_ctxs;  // contexts with batch events
+constexpr size_t kBatchStreams = 16;   // streams tracked per context (the oldest is reused)
 
 void batch_launched(ricrc_ctx* c, hipStream_t s) {
   if (!device_busy(c->device)) return;  // no service on the device (yet): nothing to hold back
-  if (!c->batch_ev) {
-    hipEvent_t ev = nullptr;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
-    std::lock_guard<std::mutex> lk(g_batch_mu);
-    c->batch_ev = ev;
-    g_batch_ctxs.push_back(c);
+  size_t i = 0;
+  while (i < c->batch_evs.size() && c->batch_evs[i].stream != s) ++i;
+  if (i == c->batch_evs.size()) {
+    if (i >= kBatchStreams) {  // (a context on very many streams: reuse the first slot)
+      i = 0;
+      c->batch_evs[0].stream = s;
+    } else {
+      hipEvent_t ev = nullptr;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+      std::lock_guard<std::mutex> lk(g_batch_mu);
+      if (c->batch_evs.empty()) g_batch_ctxs.push_back(c);
+      c->batch_evs.push_back({s, ev});
+    }
   }
-  (void)hipEventRecord(c->batch_ev, s);
+  (void)hipEventRecord(c->batch_evs[i].ev, s);
 }
 
 void batch_forget(ricrc_ctx* c) {
-  if (!c->batch_ev) return;
+  if (c->batch_evs.empty()) return;
   {
     std::lock_guard<std::mutex> lk(g_batch_mu);
     for (size_t i = 0; i < g_batch_ctxs.size(); ++i)
@@ -276,12 +293,13 @@ void batch_forget(ricrc_ctx* c) {
         break;
       }
   }
-  (void)hipEventDestroy(c->batch_ev);
-  c->batch_ev = nullptr;
+  for (auto& b : c->batch_evs) (void)hipEventDestroy(b.ev);
+  c->batch_evs.clear();
 }
 
 // Waits (at most kBatchWaitMax) until no batch launched through this library
-// is in flight on the context's device.
+// is in flight on the context's device.  (The events are queried under the
+// lock: a context destroyed on another thread frees its events under it.)
 constexpr auto kBatchWaitMax = std::chrono::milliseconds(200);
 void service_wait_batches(const ricrc_ctx* c) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -289,11 +307,15 @@ void service_wait_batches(const ricrc_ctx* c) {
     bool running = false;
     {
       std::lock_guard<std::mutex> lk(g_batch_mu);
-      for (const ricrc_ctx* x : g_batch_ctxs)
-        if (x->device == c->device && hipEventQuery(x->batch_ev) == hipErrorNotReady) {
-          running = true;
-          break;
-        }
+      for (const ricrc_ctx* x : g_batch_ctxs) {
+        if (x->device != c->device) continue;
+        for (const auto& b : x->batch_evs)
+          if (hipEventQuery(b.ev) == hipErrorNotReady) {
+            running = true;
+            break;
+          }
+        if (running) break;
+      }
     }
     if (!running || std::chrono::steady_clock::now() - t0 > kBatchWaitMax) return;
     for (int i = 0; i < 256; ++i) __builtin_ia32_pause();
@@ -307,35 +329,59 @@ void service_pause(ricrc_ctx* c) {
   if (c->svc_launched) __atomic_store_n(&c->svc->stop, 1u, __ATOMIC_RELEASE);
 }
 
-// Ragged kernel choice (icrc_ragged_mixed_kernel): each context owns one
-// word of a process-wide host-mapped block.  A ragged launch's first
-// workgroup stores into it whether its first 1024 packets hold a frame of at
-// most 128 bytes, and the context's later ragged launches run the kernel with
-// phase 0 while it is 1 (launches enqueued back to back all read what the
-// kernels finished before them wrote; a context's first ragged launch runs
-// without phase 0).  The words are never freed: a kernel launched on a
-// caller's stream may still write one after its context is destroyed (a
-// recycled word then only steers a choice, never a result).
+// Ragged kernel variant (icrc_ragged_mixed_kernel with or without the compact
+// tiny-batch phase, include/roce_icrc.h RICRC_RAGGED_*).  A variant the caller
+// set wins.  Under AUTO, host-buffer calls decide from the lengths they hold
+// (host_ragged_variant); device-resident calls follow the context's learned
+// hint: each context owns one word of a process-wide host-mapped block, a
+// ragged launch's first workgroup stores into it whether its first 1024
+// packets hold a frame of at most 128 bytes, and the context's later AUTO
+// launches run the compact kernel while it is 1 (launches enqueued back to
+// back all read what the kernels finished before them wrote; a context's
+// first one runs without the compact phase).  The words are never freed: a
+// kernel launched on a caller's stream may still write one after its context
+// is destroyed (a recycled word then only steers a choice, never a result).
 constexpr uint32_t kHintWords = 4096;
+constexpr uint32_t kTinyFrameLen = 128;  // the compact phase's longest frame
 std::mutex g_hint_mu;
 uint32_t* g_hints = nullptr;
 uint32_t g_hint_next = 0;
+bool g_hint_failed = false;  // the block could not be allocated: no hints in this process
 
 uint32_t* hint_word() {
   std::lock_guard<std::mutex> lk(g_hint_mu);
+  if (g_hint_failed) return nullptr;
   if (!g_hints) {
     void* h = nullptr;
-    if (hipHostMalloc(&h, kHintWords * 64u, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-      return nullptr;  // (no hint: the kernel without phase 0, still exact)
+    if (hipHostMalloc(&h, kHintWords * 64u, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      g_hint_failed = true;  // (no hint: AUTO device launches run without the compact phase, still exact)
+      return nullptr;
+    }
     std::memset(h, 0, kHintWords * 64u);
     g_hints = (uint32_t*)h;
   }
   return g_hints + 16u * (g_hint_next++ % kHintWords);  // (one 64-byte line each)
 }
 
+// AUTO for a batch whose lengths are on the host: the compact phase pays for
+// packed runs of tiny frames, so count the 64-frame groups whose frames are
+// all at most 128 bytes; at least 1/16 of the groups selects it.
+int host_ragged_variant(const uint32_t* lens, uint32_t n) {
+  uint32_t groups = 0, tiny = 0;
+  for (uint32_t g = 0; g < n; g += 64, ++groups) {
+    const uint32_t e = n - g < 64 ? n : g + 64;
+    uint32_t k = g;
+    while (k < e && lens[k] <= kTinyFrameLen) ++k;
+    tiny += k == e ? 1u : 0u;
+  }
+  return tiny && 16u * tiny >= groups ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
+}
+
+// `host_lens`: the batch's lengths when the caller passed them on the host
+// (AUTO then decides from them), else nullptr.
 int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint32_t* lens,
            uint64_t stride, uint32_t len, uint32_t n, uint32_t* icrc, uint8_t* status, uint8_t* ok,
-           bool ragged, bool verify, int log2g, hipStream_t s) {
+           bool ragged, bool verify, int log2g, hipStream_t s, const uint32_t* host_lens = nullptr) {
   service_pause(c);
   ricrc::IcrcArgs a{};
   a.frames = frames;
@@ -357,12 +403,17 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
   } else {
     if (!ragged && c->num_cus <= ricrc::kMaxClaimBlocks) a.claims = claim_region(c, s, &a.epoch);
     bool compact = false;
-    if (ragged) {
+    if (ragged && n > 0) {
       if (!c->tiny_hint) c->tiny_hint = hint_word();
-      if (c->tiny_hint) {
-        compact = __atomic_load_n(c->tiny_hint, __ATOMIC_ACQUIRE) != 0u;
-        a.tiny_hint = c->tiny_hint;
-      }
+      a.tiny_hint = c->tiny_hint;  // (kept current under every variant, for AUTO)
+      int v = c->ragged_variant;
+      if (v == RICRC_RAGGED_AUTO)
+        v = host_lens ? host_ragged_variant(host_lens, n)
+            : c->tiny_hint && __atomic_load_n(c->tiny_hint, __ATOMIC_ACQUIRE) != 0u ? RICRC_RAGGED_COMPACT
+                                                                                    : RICRC_RAGGED_SORTED;
+      // (only the mixed-width kernel has the compact phase)
+      compact = v == RICRC_RAGGED_COMPACT && ricrc::ragged_has_compact(log2g);
+      c->last_ragged = compact ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
     }
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s, compact));
   }
@@ -418,7 +469,7 @@ int host_ragged_staged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,
   HIP_TRY(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
   rc = launch(c, d, (const uint64_t*)(d + o_offs), (const uint32_t*)(d + o_lens), 0, 0, n,
               (uint32_t*)(d + o_icrc), d + o_st, verify ? d + o_ok : nullptr, true, verify,
-              ragged_log2g(c, mean_len(lens, n)), c->stream);
+              ragged_log2g(c, mean_len(lens, n)), c->stream, lens);
   if (rc) return rc;
   const size_t out_end = verify ? o_ok + n : o_st + n;
   HIP_TRY(hipMemcpyAsync(h + o_icrc, d + o_icrc, out_end - o_icrc, hipMemcpyDeviceToHost,
@@ -472,7 +523,7 @@ int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const 
       hipMemcpyAsync(c->d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
   rc = launch(c, c->d_frames, c->d_offs, c->d_lens, 0, 0, n, c->d_icrc, c->d_status,
               verify ? c->d_ok : nullptr, true, verify, ragged_log2g(c, mean_len(lens, n)),
-              c->stream);
+              c->stream, lens);
   if (rc) return rc;
   if (icrc_out)
     HIP_TRY(hipMemcpyAsync(icrc_out, c->d_icrc, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -878,7 +929,7 @@ struct MultiBatch {
   bool verify;
 };
 
-int multi_shard(ricrc_ctx* c, const MultiBatch& b, uint32_t d) {
+int multi_shard_run(ricrc_ctx* c, const MultiBatch& b, uint32_t d) {
   if (d >= b.n) return RICRC_OK;
   uint32_t maxlen = 0;
   for (uint64_t i = d; i < b.n; i += b.stride) maxlen = b.lens[i] > maxlen ? b.lens[i] : maxlen;
@@ -938,7 +989,7 @@ int multi_shard(ricrc_ctx* c, const MultiBatch& b, uint32_t d) {
     uint8_t* d_st = dv + o_out + 4ull * m;
     rc = launch(c, dv, (const uint64_t*)(dv + o_desc), (const uint32_t*)(dv + o_desc + 8ull * m), 0,
                 0, m, d_icrc, d_st, b.verify ? d_st + m : nullptr, true, b.verify,
-                ragged_log2g(c, (uint32_t)(pos / m)), c->stream);
+                ragged_log2g(c, (uint32_t)(pos / m)), c->stream, ls);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(h + o_out, dv + o_out, (b.verify ? 6ull : 5ull) * m,
                            hipMemcpyDeviceToHost, c->stream));
@@ -949,6 +1000,18 @@ int multi_shard(ricrc_ctx* c, const MultiBatch& b, uint32_t d) {
   rc = scatter(s);
   if (rc) return rc;
   return scatter(s ^ 1);
+}
+
+// A shard that fails part-way may leave copies of the staging blocks queued
+// on the context's stream: drain them, so the next call (or multi_ensure
+// freeing a block) never meets a block that is still being copied.
+int multi_shard(ricrc_ctx* c, const MultiBatch& b, uint32_t d) {
+  const int rc = multi_shard_run(c, b, d);
+  if (rc != RICRC_OK) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+  }
+  return rc;
 }
 
 int batch_multi(ricrc_ctx** ctxs, int nctx, const uint8_t* frames, size_t frames_bytes,
@@ -1087,6 +1150,18 @@ int ricrc_ctx_set_lanes_per_packet(ricrc_ctx* c, int lanes) {
 }
 
 void* ricrc_ctx_stream(ricrc_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int ricrc_ctx_set_ragged_variant(ricrc_ctx* c, int variant) {
+  if (!c || variant < RICRC_RAGGED_AUTO || variant > RICRC_RAGGED_SORTED) return RICRC_EINVAL;
+  c->ragged_variant = variant;
+  return RICRC_OK;
+}
+
+int ricrc_ctx_last_ragged_variant(ricrc_ctx* c, int* variant_out) {
+  if (!c || !variant_out) return RICRC_EINVAL;
+  *variant_out = c->last_ragged;
+  return RICRC_OK;
+}
 
 int ricrc_lanes_for_len(ricrc_ctx* c, uint32_t len) {
   if (!c) return RICRC_EINVAL;

@@ -54,6 +54,10 @@ constexpr int kMaxClaimBlocks = 1024;
 // Builds the table image on the host (kTableWords words).
 void build_table_image(uint32_t* out);
 
+// Ragged launches at 8 lanes per packet run the mixed-width kernel, the one
+// built with and without the compact tiny-batch phase (`compact` below).
+constexpr bool ragged_has_compact(int log2g) { return log2g == 3; }
+
 // Enqueues the ICRC kernel; returns a hipError_t.
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
                        hipStream_t stream, bool compact = false);

@@ -45,6 +45,9 @@ SEG_SIGNALED, SEG_SOLICITED = 0x1, 0x2
 # fault kinds (RICRC_FAULT_*)
 FAULT_ICRC, FAULT_PAYLOAD, FAULT_MASKED = 0x1, 0x2, 0x4
 
+# ragged-kernel variants (RICRC_RAGGED_*, ABI 5)
+RAGGED_AUTO, RAGGED_COMPACT, RAGGED_SORTED = 0, 1, 2
+
 # struct ricrc_seg_wr (include/roce_icrc.h), 80 bytes, as a numpy record so
 # large WR batches are built vectorised
 SEG_WR_DTYPE = np.dtype([
@@ -80,6 +83,8 @@ _SIGNATURES = {
     "ricrc_ctx_destroy": (None, [_vp]),
     "ricrc_ctx_set_lanes_per_packet": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ricrc_ctx_stream": (_vp, [_vp]),
+    "ricrc_ctx_set_ragged_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "ricrc_ctx_last_ragged_variant": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "ricrc_ctx_set_service": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "ricrc_ctx_service_times": (ctypes.c_int, [_vp, _vp]),
     "ricrc_compute_one": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, _vp]),
@@ -331,6 +336,21 @@ class IcrcEngine:
         t = np.zeros(3, np.uint64)
         self._check("ricrc_ctx_service_times", self.lib.ricrc_ctx_service_times(self.ctx, _ptr(t)))
         return float(int(t[1]) - int(t[0])) * 0.01, int(t[2])
+
+    def set_ragged_variant(self, variant: int) -> None:
+        """RAGGED_AUTO (default), RAGGED_COMPACT (the ragged kernel with the
+        compact tiny-batch phase: packed ACK / NAK runs) or RAGGED_SORTED
+        (without it) for this engine's ragged launches (include/roce_icrc.h)."""
+        self._check("ricrc_ctx_set_ragged_variant",
+                    self.lib.ricrc_ctx_set_ragged_variant(self.ctx, variant))
+
+    def last_ragged_variant(self) -> int:
+        """The variant the engine's last ragged kernel launch ran
+        (RAGGED_COMPACT / RAGGED_SORTED; RAGGED_AUTO before any)."""
+        v = ctypes.c_int(-1)
+        self._check("ricrc_ctx_last_ragged_variant",
+                    self.lib.ricrc_ctx_last_ragged_variant(self.ctx, ctypes.byref(v)))
+        return v.value
 
     def lanes_for_len(self, length: int) -> int:
         return self.lib.ricrc_lanes_for_len(self.ctx, length)

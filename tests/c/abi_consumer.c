@@ -51,9 +51,24 @@ static int gpu_leg(ricrc_ctx* ctx, int ndev) {
     uint32_t mm[3] = {0, 0, 0};
     if (ricrc_verify_batch_multi(same, 2, buf, sizeof buf, offs, lens, 3, okm, mm, NULL) !=
         RICRC_OK)
-      return 29;
+      return 31;
     if (okm[0] != 1 || okm[1] != 0 || okm[2] != 1 || mm[0] != out[0] || mm[1] != out[1])
-      return 30;
+      return 32;
+  }
+  {  /* ABI 5: the ragged variant of a context; host batches of 3 frames go to
+      * the resident wave, so the kernel path is forced with the service off */
+    int v = -1;
+    if (ricrc_ctx_set_ragged_variant(ctx, 3) != RICRC_EINVAL) return 33;
+    if (ricrc_ctx_last_ragged_variant(ctx, &v) != RICRC_OK || v != RICRC_RAGGED_AUTO) return 34;
+    if (ricrc_ctx_set_service(ctx, 0) != RICRC_OK) return 35;
+    if (ricrc_ctx_set_ragged_variant(ctx, RICRC_RAGGED_COMPACT) != RICRC_OK) return 36;
+    uint32_t vc[3] = {0, 0, 0};
+    if (ricrc_compute_batch(ctx, buf, sizeof buf, offs, lens, 3, vc, NULL) != RICRC_OK) return 37;
+    if (vc[0] != out[0] || vc[1] != out[1] || vc[2] != out[2]) return 38;
+    /* (48-B frames on the host run the one-lane ragged kernel: no compact phase) */
+    if (ricrc_ctx_last_ragged_variant(ctx, &v) != RICRC_OK || v != RICRC_RAGGED_SORTED) return 41;
+    if (ricrc_ctx_set_ragged_variant(ctx, RICRC_RAGGED_AUTO) != RICRC_OK) return 39;
+    if (ricrc_ctx_set_service(ctx, 1000) != RICRC_OK) return 40;
   }
   if (ndev >= 2) {
     ricrc_ctx* c2 = NULL;
@@ -71,6 +86,7 @@ static int gpu_leg(ricrc_ctx* ctx, int ndev) {
 int main(void) {
   if (ricrc_abi_version() != RICRC_ABI_VERSION) return 1;
   if (strcmp(ricrc_strerror(RICRC_EINVAL), "invalid argument") != 0) return 2;
+  if (ricrc_ctx_set_ragged_variant(NULL, RICRC_RAGGED_COMPACT) != RICRC_EINVAL) return 9;
   /* Util.compute_wr_pkt_num (src/roce_util.py:183-185): a 10000-byte SEND at
    * PMTU 4096 is 3 packets, a zero-length one 1 packet */
   ricrc_seg_wr wrs[2];

@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_errors():
     lib = E.load_library()
-    assert lib.ricrc_abi_version() == 4
+    assert lib.ricrc_abi_version() == 5
     assert lib.ricrc_strerror(0) == b"ok"
     assert lib.ricrc_strerror(-22) == b"invalid argument"
     assert lib.ricrc_strerror(-19) == b"no usable gfx950 device"
@@ -85,7 +85,7 @@ def test_header_is_plain_c_and_links(tmp_path):
     if torch.cuda.is_available():
         pytest.skip("GPU visible: the run leg is tests/test_gpu_capi.py")
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
-    assert out.startswith("abi 4 ok: 4 packets, slot 4224"), out
+    assert out.startswith("abi 5 ok: 4 packets, slot 4224"), out
     assert "gpu leg skipped" in out
 
 

@@ -14,5 +14,5 @@ def test_c_program_drives_the_gpu(tmp_path):
     exe = build_abi_consumer(tmp_path)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, f"abi_consumer failed check {r.returncode}: {r.stdout}{r.stderr}"
-    assert r.stdout.startswith("abi 4 ok: 4 packets, slot 4224"), r.stdout
+    assert r.stdout.startswith("abi 5 ok: 4 packets, slot 4224"), r.stdout
     assert "ctx_create 0, gpu leg ok" in r.stdout, r.stdout

@@ -229,3 +229,58 @@ def test_plain_bench_gpus2_launches_its_own_ranks():
     cpu = line["cpu_baseline"]
     assert cpu is not None and cpu["parity_mismatches_vs_gpu"] == 0
     assert cpu["sample"].startswith("rank 0's shard (40000 packets of 80000)")
+
+
+
+# Ranks of the full-size rehearsal on this box: 4.  The 8-rank launch is the
+# driver's (its 8-GPU scaling run); the pool's rules keep `bench.py --gpus 8`
+# out of our own GPU calls, so 8 ranks are rehearsed on the CPU over gloo
+# (tests/test_dist.py, the same shard split and per-rank gathers).
+REHEARSAL_RANKS = 4
+
+
+@pytest.mark.timeout(900)
+def test_bench_multi_rank_cfg4_rehearsal_full_size(tmp_path):
+    """BASELINE config 4 end to end at full per-rank size, launched as the
+    driver launches it (plain `python bench.py --gpus N`, bench.py starting its
+    own ranks): ONE stream of N * 2^20 4140-B packets seeded 0x1C2C0004,
+    packet i on rank i mod N, 2^20 packets per rank.  With fewer than N GPUs
+    every rank is pinned to device 0 (ROCE_ICRC_BENCH_DEVICE): the N-rank path
+    -- rendezvous, per-rank shards, the N-way gathers, rank 0's CPU baseline
+    while the others wait -- not a scaling number.  Every rank's sampled
+    parity against the oracle, its device check, and the per-rank numbers of
+    the line."""
+    N = REHEARSAL_RANKS
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    if _ndev() < N:
+        env["ROCE_ICRC_BENCH_DEVICE"] = "0"
+    out_dir = ROOT / "gpurun_out"
+    out_dir.mkdir(exist_ok=True)
+    log = out_dir / f"rehearsal_n{N}.log"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(N), "--steps", "5", "--warmup",
+           "2", "--no-e2e"]
+    with open(log, "w") as err:  # (the ranks' stderr: progress of a long run)
+        r = subprocess.run(cmd, env=env, cwd=str(ROOT), stdout=subprocess.PIPE, stderr=err,
+                           text=True, timeout=840)
+    assert r.returncode == 0, log.read_text()[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    (out_dir / f"rehearsal_n{N}.json").write_text(lines[0] + "\n")
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == N and line["config"]["workload"].startswith("cfg4")
+    assert line["config"]["packets_per_gpu"] == 1 << 20
+    assert line["parity"]["mismatches_per_rank"] == [0] * N
+    assert line["parity"]["sampled_per_rank"] == [1 << 16] * N
+    assert line["checks"]["pass"]
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["parity_mismatches_vs_gpu"] == 0
+    assert cpu["sample"].startswith(f"rank 0's shard ({1 << 20} packets of {N << 20})")
+    for k in ("per_rank_GiBps", "per_rank_kernel_ms", "per_rank_kernel_GiBps", "per_rank_device"):
+        assert len(line[k]) == N, k
+    assert all(x > 0 for x in line["per_rank_GiBps"] + line["per_rank_kernel_ms"])
+    # the aggregate: all ranks' covered bytes over the slowest rank's time
+    cov = line["config"]["covered_bytes_per_gpu"]
+    agg = N * cov / (line["ms_per_step"] * 1e-3) / 2**30
+    assert abs(line["value"] - agg) < 0.01 * line["value"]
+    assert min(line["per_rank_GiBps"]) * N <= line["value"] * 1.01

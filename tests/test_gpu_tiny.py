@@ -11,6 +11,7 @@ from conftest import oracle_batch
 
 pytestmark = pytest.mark.gpu
 
+from roce_icrc import engine as E  # noqa: E402
 from roce_icrc import synth  # noqa: E402
 
 
@@ -33,24 +34,35 @@ def _ragged(lens, seed):
     return buf, offs, lens
 
 
+VARIANTS = (E.RAGGED_COMPACT, E.RAGGED_SORTED)
+
+
 def _run(engine, buf, offs, lens, verify=False, flip_every=0):
+    """Every launch under both ragged-kernel variants, chosen explicitly
+    (ricrc_ctx_set_ragged_variant): the kernel with the compact tiny-batch
+    phase and the one without must give the same words and verdicts, and each
+    launch must report the variant it was asked for -- whatever ran before on
+    the (session-scoped) engine."""
     torch = pytest.importorskip("torch")
     n = lens.size
     d = torch.from_numpy(buf).cuda()
     do = torch.from_numpy(offs.view(np.int64)).cuda()
     dl = torch.from_numpy(lens.view(np.int32)).cuda()
     out = torch.zeros(n, dtype=torch.int32, device="cuda")
-    # every launch twice: the context's first look at tiny frames may run the
-    # ragged kernel without phase 0, the next runs the one with it (hint word,
-    # icrc_capi.cpp hint_word); both must give the same words
-    engine.compute_batch_dev(d, do, dl, n, out)
-    torch.cuda.synchronize()
-    first = out.cpu().numpy().view(np.uint32).copy()
-    out.zero_()
-    engine.compute_batch_dev(d, do, dl, n, out)
-    torch.cuda.synchronize()
-    got = out.cpu().numpy().view(np.uint32).copy()
-    np.testing.assert_array_equal(first, got)
+    words = []
+    try:
+        for v in VARIANTS:
+            engine.set_ragged_variant(v)
+            out.zero_()
+            engine.compute_batch_dev(d, do, dl, n, out)
+            assert engine.last_ragged_variant() == v
+            torch.cuda.synchronize()
+            words.append(out.cpu().numpy().view(np.uint32).copy())
+    finally:
+        engine.set_ragged_variant(E.RAGGED_AUTO)
+    np.testing.assert_array_equal(words[0], words[1])
+    got = words[0]
+    out.copy_(torch.from_numpy(got.view(np.int32)))
     if not verify:
         return got, None
     # trailers from the GPU words, every flip_every-th frame corrupted
@@ -62,15 +74,19 @@ def _run(engine, buf, offs, lens, verify=False, flip_every=0):
         pos = torch.from_numpy((offs[bad] + 40).astype(np.int64)).cuda()
         d[pos] ^= 1
     ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    engine.verify_batch_dev(d, do, dl, n, ok)
-    torch.cuda.synchronize()
-    first_ok = ok.cpu().numpy().astype(bool)
-    ok.zero_()
-    engine.verify_batch_dev(d, do, dl, n, ok)
-    torch.cuda.synchronize()
-    ok_now = ok.cpu().numpy().astype(bool)
-    np.testing.assert_array_equal(first_ok, ok_now)
-    return got, (ok_now, bad)
+    oks = []
+    try:
+        for v in VARIANTS:
+            engine.set_ragged_variant(v)
+            ok.zero_()
+            engine.verify_batch_dev(d, do, dl, n, ok)
+            assert engine.last_ragged_variant() == v
+            torch.cuda.synchronize()
+            oks.append(ok.cpu().numpy().astype(bool))
+    finally:
+        engine.set_ragged_variant(E.RAGGED_AUTO)
+    np.testing.assert_array_equal(oks[0], oks[1])
+    return got, (oks[0], bad)
 
 
 def test_ack_sized_batch_device_resident(engine):
@@ -119,8 +135,10 @@ def test_window_sequences_switch_the_table_half(engine):
     np.testing.assert_array_equal(got, want)
 
 
-def _dev_compute(engine, buf, offs, lens):
-    """compute_batch_dev with status: (icrc, status) as numpy."""
+def _dev_compute(engine, buf, offs, lens, variant=E.RAGGED_COMPACT):
+    """compute_batch_dev with status: (icrc, status) as numpy, on the ragged
+    kernel variant asked for (default: the one with the compact phase, whose
+    tests these are -- independent of what the engine ran before)."""
     torch = pytest.importorskip("torch")
     n = lens.size
     d = torch.from_numpy(buf).cuda()
@@ -128,7 +146,12 @@ def _dev_compute(engine, buf, offs, lens):
     dl = torch.from_numpy(lens.view(np.int32)).cuda()
     out = torch.zeros(n, dtype=torch.int32, device="cuda")
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    engine.compute_batch_dev(d, do, dl, n, out, st)
+    engine.set_ragged_variant(variant)
+    try:
+        engine.compute_batch_dev(d, do, dl, n, out, st)
+        assert engine.last_ragged_variant() == variant
+    finally:
+        engine.set_ragged_variant(E.RAGGED_AUTO)
     torch.cuda.synchronize()
     return out.cpu().numpy().view(np.uint32).copy(), st.cpu().numpy().copy()
 
@@ -187,6 +210,9 @@ def test_compact_batches_malformed_and_options(engine):
     want = np.array([o.icrc_of_frame(f) for f in frames], np.uint32)
     got, st = _dev_compute(engine, buf, offs, lens)
     np.testing.assert_array_equal(got, want)
+    got_s, st_s = _dev_compute(engine, buf, offs, lens, E.RAGGED_SORTED)
+    np.testing.assert_array_equal(got_s, want)
+    np.testing.assert_array_equal(st_s, st)
     e8 = IcrcEngine(0, lanes=8)
     try:
         got8, st8 = _dev_compute(e8, buf, offs, lens)
@@ -221,15 +247,17 @@ def test_compact_test_rejects_unsafe_layouts(engine):
         buf[d_:d_ + 48] = buf[s_:s_ + 48]
     offs[b(4)] = dst.astype(np.uint64)
     want, _ = oracle_batch(buf, offs, lens)
-    got, _ = _dev_compute(engine, buf, offs, lens)
-    np.testing.assert_array_equal(got, want)
+    for v in VARIANTS:
+        got, _ = _dev_compute(engine, buf, offs, lens, v)
+        np.testing.assert_array_equal(got, want)
     # a 300-B frame between ACKs: that batch is not compact, its neighbours are
     lens2 = np.full(n, 48, np.uint32)
     lens2[64 * 5 + 7] = 300
     buf2, offs2, lens2 = _ragged(lens2, 6)
     want2, _ = oracle_batch(buf2, offs2, lens2)
-    got2, _ = _dev_compute(engine, buf2, offs2, lens2)
-    np.testing.assert_array_equal(got2, want2)
+    for v in VARIANTS:
+        got2, _ = _dev_compute(engine, buf2, offs2, lens2, v)
+        np.testing.assert_array_equal(got2, want2)
 
 
 def test_compact_rounds_between_sorted_rounds(engine):
@@ -261,7 +289,8 @@ def test_compact_rounds_between_sorted_rounds(engine):
 def test_bench_ack_workload_line():
     """bench.py --workload ack (device-resident ragged ACK frames, the compact
     tiny-batch phase): the line's device check and per-rank sampled parity
-    pass, with the ragged roofline accounting (frame + descriptor + word)."""
+    pass; SURVEY 8(d)'s roofline accounting (frame + word, the 12-B
+    descriptors reported apart); every timed launch on the compact kernel."""
     import json
     import os
     import subprocess
@@ -275,7 +304,9 @@ def test_bench_ack_workload_line():
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["checks"]["pass"] and d["config"]["packets_per_gpu"] == 300000
     assert all(m == 0 for m in d["parity"]["mismatches_per_rank"])
-    assert d["roofline"]["alg_bytes_per_launch"] == 300000 * (44 + 16)
+    assert d["roofline"]["alg_bytes_per_launch"] == 300000 * (44 + 4)
+    assert d["roofline"]["descriptor_bytes_per_launch"] == 300000 * 12
+    assert d["config"]["ragged_kernel"].startswith("compact")
 
 
 def test_kernel_choice_follows_the_frames():
@@ -299,3 +330,59 @@ def test_kernel_choice_follows_the_frames():
     finally:
         eng.close()
 
+
+
+def test_variant_named_per_launch_when_batches_alternate():
+    """ABI 5: a context whose device-resident batches alternate composition --
+    mixed-MTU data (src/roce_v2.py:327-372) and packed ACK runs
+    (src/roce_rq.py:767-853) -- names the ragged variant per call.  Launches
+    enqueued back to back without a synchronisation each run the variant
+    named (ricrc_ctx_last_ragged_variant), every word bit-exact; and the ACK
+    batches run measurably faster on the compact variant than on the sorted
+    one (HIP events on the launch stream), so the two really are different
+    kernels."""
+    torch = pytest.importorskip("torch")
+    from roce_icrc import IcrcEngine
+    eng = IcrcEngine(0)
+    try:
+        data = synth.mixed_mtu_frames(20000, seed=7)
+        ack = synth.mixed_mtu_frames(1 << 22, mtus=(4,), opcode=0x11, seed=8)
+        dev = []
+        for buf, offs, lens in (data, ack):
+            dev.append((torch.from_numpy(buf).cuda(), torch.from_numpy(offs.view(np.int64)).cuda(),
+                        torch.from_numpy(lens.view(np.int32)).cuda(), lens.size))
+        want = [oracle_batch(*data)[0], oracle_batch(*ack)[0]]
+        plan = [(0, E.RAGGED_SORTED), (1, E.RAGGED_COMPACT)] * 3 + [(1, E.RAGGED_SORTED),
+                                                                     (0, E.RAGGED_COMPACT)]
+        outs, ran = [], []
+        s = torch.cuda.current_stream()
+        for which, v in plan:
+            d, do, dl, n = dev[which]
+            out = torch.zeros(n, dtype=torch.int32, device="cuda")
+            eng.set_ragged_variant(v)
+            eng.compute_batch_dev(d, do, dl, n, out, stream=s.cuda_stream)
+            ran.append(eng.last_ragged_variant())
+            outs.append(out)
+        torch.cuda.synchronize()
+        assert ran == [v for _, v in plan]
+        for (which, v), out in zip(plan, outs):
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want[which],
+                                          err_msg=f"batch {which} variant {v}")
+        # the ACK batch, 5 launches per variant, alternating groups
+        d, do, dl, n = dev[1]
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ms = {E.RAGGED_COMPACT: [], E.RAGGED_SORTED: []}
+        for _ in range(3):
+            for v in (E.RAGGED_COMPACT, E.RAGGED_SORTED):
+                eng.set_ragged_variant(v)
+                for _ in range(5):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(s)
+                    eng.compute_batch_dev(d, do, dl, n, out, stream=s.cuda_stream)
+                    b.record(s)
+                    ms[v].append((a, b))
+        torch.cuda.synchronize()
+        t = {v: float(np.median([a.elapsed_time(b) for a, b in evs])) for v, evs in ms.items()}
+        assert t[E.RAGGED_COMPACT] < 0.9 * t[E.RAGGED_SORTED], t
+    finally:
+        eng.close()
