@@ -484,10 +484,7 @@ int host_ragged_staged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes,
 int service_burst(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offsets,
                   const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,
                   uint8_t* ok_out, bool verify);
-#ifndef RICRC_SVC_BURST_ROUTE
-#define RICRC_SVC_BURST_ROUTE 64
-#endif
-constexpr uint32_t kSvcBurstRoute = RICRC_SVC_BURST_ROUTE;  // host batches up to this many frames
+constexpr uint32_t kSvcBurstRoute = 64;  // host batches up to this many frames
 
 int host_ragged(ricrc_ctx* c, const uint8_t* frames, size_t frames_bytes, const uint64_t* offsets,
                 const uint32_t* lens, uint32_t n, uint32_t* icrc_out, uint8_t* status_out,

@@ -18,10 +18,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-#ifndef RICRC_UNROLL
-#define RICRC_UNROLL 4
-#endif
-constexpr int kUnroll = RICRC_UNROLL;  // iterations per body block (dwordx4 loads in flight per lane)
+constexpr int kUnroll = 4;  // iterations per body block (dwordx4 loads in flight per lane)
 
 __device__ __forceinline__ uint32_t lds_rd(uint32_t byte_addr) {
   return *(const lds_u32*)(uintptr_t)byte_addr;
@@ -117,10 +114,7 @@ __device__ __forceinline__ void stg8(uint8_t* p, uint32_t v) {
 }
 // Scattered per-packet words and flags: default policy (sc1 measured 4-5 %
 // and nt 2-10 % slower on cfg3's verdict bytes, both neutral on cfg2).
-#ifndef RICRC_PKT_STORE_POL
-#define RICRC_PKT_STORE_POL 0
-#endif
-constexpr int kPktStorePol = RICRC_PKT_STORE_POL;
+constexpr int kPktStorePol = 0;
 
 // Batch kernels announce themselves to the per-packet service waves resident
 // on the same device (icrc_service_kernel): thread 0 of every workgroup

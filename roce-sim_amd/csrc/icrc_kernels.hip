@@ -58,15 +58,9 @@ namespace {
 // 64 KiB in flight per CU and 6.70 with 128 KiB (scratch/read_ceiling.hip);
 // cfg2 at 12 waves +2 % (6050 -> 6179 GiB/s, 3 A/B rounds; 10 waves +1.7 %,
 // 8 waves -1 %).
-#ifndef RICRC_THREADS
-#define RICRC_THREADS 1024
-#endif
-#ifndef RICRC_STRIDED_THREADS
-#define RICRC_STRIDED_THREADS 768
-#endif
-constexpr int kIcrcThreads = RICRC_THREADS;  // ragged kernel
+constexpr int kIcrcThreads = 1024;  // ragged kernel
 constexpr int kIcrcWaves = kIcrcThreads / 64;
-constexpr int kStridedThreads = RICRC_STRIDED_THREADS;
+constexpr int kStridedThreads = 768;
 constexpr int kStridedWaves = kStridedThreads / 64;
 
 constexpr uint32_t kPktBadLen = 0x01, kPktNotIpv4 = 0x02, kPktNotUdp = 0x04,
@@ -317,16 +311,9 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
 // sends loads out ahead of other waves' folds and the HBM queue stays full:
 // cfg2 +0.5 % (6012 -> 6042 GiB/s, 3 A/B rounds on each of two boxes;
 // priority 2 the same, cfg3 and the segmentation kernel neutral, also raising
-// it for a packet's first batch measured worse), cfg5 +2.5-12 %.  0 disables.
-#ifndef RICRC_SETPRIO
-#define RICRC_SETPRIO 3
-#endif
-__device__ __forceinline__ void body_prio_hi() {
-  if constexpr (RICRC_SETPRIO > 0) __builtin_amdgcn_s_setprio(RICRC_SETPRIO);
-}
-__device__ __forceinline__ void body_prio_lo() {
-  if constexpr (RICRC_SETPRIO > 0) __builtin_amdgcn_s_setprio(0);
-}
+// it for a packet's first batch measured worse), cfg5 +2.5-12 %.
+__device__ __forceinline__ void body_prio_hi() { __builtin_amdgcn_s_setprio(3); }
+__device__ __forceinline__ void body_prio_lo() { __builtin_amdgcn_s_setprio(0); }
 
 // Fold, combine, check and emit one packet whose first batch is in `b`.
 template <int LOG2G, bool VERIFY, class K = MainKeys, uint32_t LUT = kFixLut<LOG2G, MainKeys>>
@@ -448,22 +435,13 @@ __device__ __forceinline__ void emit_packet(const IcrcArgs& a, const Pkt& p, con
 // sessions, profiles/r03q_tail_ab*.txt): 1/2 0.6417, 1/4 0.6309, 1/8
 // 0.6246 (+1.0 %), 1/16 0.6353, 1/32 0.6364; 2 victims at 1/8 0.6274, 8
 // victims at 1/4 0.6324.
-#ifndef RICRC_TAIL_DIV
-#define RICRC_TAIL_DIV 8
-#endif
-constexpr uint32_t kTailDiv = RICRC_TAIL_DIV;
-#ifndef RICRC_MAX_VICTIMS
-#define RICRC_MAX_VICTIMS 4
-#endif
-constexpr uint32_t kMaxVictims = RICRC_MAX_VICTIMS;
+constexpr uint32_t kTailDiv = 8;
+constexpr uint32_t kMaxVictims = 4;
 
 // Cache policy of the block's output run (out_store128): default.  The run
 // goes out at the end of the block, when the rest of the chip still streams;
 // sc1 measured 0.5 % slower on cfg2 (3 A/B rounds).
-#ifndef RICRC_STRIDED_OUT_POL
-#define RICRC_STRIDED_OUT_POL 0
-#endif
-constexpr int kStridedOutPol = RICRC_STRIDED_OUT_POL;
+constexpr int kStridedOutPol = 0;
 
 // Fixed-size frames at frames + i * stride.
 template <int LOG2G, bool VERIFY>
@@ -757,35 +735,16 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_kernel(IcrcArgs a
 // Mul(128) staged into the G = 4 half of the Keys8 rows, and the G = 4 table
 // is restaged for the rest of the window (barriers around both restages; a
 // window of tiny frames only keeps Mul(128) for the next window).
-#ifndef RICRC_RAGGED_MIXED
-#define RICRC_RAGGED_MIXED 1
-#endif
 // Frames of at most this many bytes (the claim's last, i.e. longest, sorted
 // frame) run as G = 4 sets.
-#ifndef RICRC_MIXED_SHORT_LEN
-#define RICRC_MIXED_SHORT_LEN 600
-#endif
-constexpr uint32_t kMixedShortLen = RICRC_MIXED_SHORT_LEN;
-#ifndef RICRC_MIXED_TINY_LEN
-#define RICRC_MIXED_TINY_LEN 128
-#endif
-#ifndef RICRC_MIXED_TINY_MIN
-#define RICRC_MIXED_TINY_MIN 256
-#endif
-constexpr uint32_t kTinyLen = RICRC_MIXED_TINY_LEN;  // frames run as G = 1 sets (0: never)
-constexpr int kTinyMin = RICRC_MIXED_TINY_MIN;       // tiny frames a window needs for phase A
-// Ragged launches: workgroups per CU over the whole launch (one resident at a
-// time: the LDS holds one); more than one lets the dispatcher balance CUs.
-#ifndef RICRC_RAGGED_BLOCKS_PER_CU
-#define RICRC_RAGGED_BLOCKS_PER_CU 1
-#endif
+constexpr uint32_t kMixedShortLen = 600;
+constexpr uint32_t kTinyLen = 128;  // frames run as G = 1 sets (0: never)
+constexpr int kTinyMin = 256;       // tiny frames a window needs for phase A
 using MixedKeysL = Keys8T<0>;  // Mul(1024), G = 8
 using MixedKeysS = Keys8T<1>;  // Mul(512), G = 4
 constexpr uint32_t kMixedLut = kFixLut<3, MixedKeysL>;  // after the 4 combine sets
-#ifndef RICRC_MIXED_WINDOW
-#define RICRC_MIXED_WINDOW 8192
-#endif
-using MixedLds = WindowLds<kMixedLut + 256u, RICRC_MIXED_WINDOW>;
+constexpr int kMixedWindow = 8192;  // packets per window (the sort's LDS arrays)
+using MixedLds = WindowLds<kMixedLut + 256u, kMixedWindow>;
 
 // The four-chain fold of the small kernel (and the ragged kernel's compact
 // tiny batches) over dwords [0, n) of one frame,
@@ -844,12 +803,6 @@ __device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb
   return fold_masked4<GLOBAL, K, COMB, CH>(f, pb, ihl, n);
 }
 
-// Window sort: wave-aggregated histogram / scatter atomics (A/B switch).
-#ifndef RICRC_HIST_AGG
-#define RICRC_HIST_AGG 0
-#endif
-constexpr bool kHistAgg = RICRC_HIST_AGG != 0;
-
 // Compact tiny batches ("phase 0", round 4).  The responder's frames (ACK /
 // NAK / atomic ack, 48-56 B, src/roce_rq.py:767-853) come in packed runs: 64
 // consecutive window packets whose frames lie in order, without overlap,
@@ -873,10 +826,7 @@ static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
 // a batch's words (one coalesced 256-B store per wave) are written
 // non-temporally: ACK bench +1.6-3 % over 3 A/B rounds against the default
 // policy (whole-library nt builds: cfg3 neutral; sc1 -1.5 %; profiles/r04x)
-#ifndef RICRC_COMPACT_STORE_POL
-#define RICRC_COMPACT_STORE_POL 2
-#endif
-constexpr int kCompactStorePol = RICRC_COMPACT_STORE_POL;
+constexpr int kCompactStorePol = 2;
 // the window's compact batches, entry wave * KR + round: {span start (u64), -, span bytes}
 constexpr uint32_t kCompactList = MixedLds::kBytes;
 constexpr uint32_t kMixedLdsBytes = kCompactList + 16u * (uint32_t)(MixedLds::kWindow / 64);
@@ -1171,22 +1121,10 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
         }
       }
       keys[r] = compact ? -1 : key;
+      // (one LDS atomic per packet: wave-aggregated adds, one per distinct
+      // key, measured no faster)
       const bool counted = i < cnt && !compact;
-      if constexpr (kHistAgg) {
-        // one LDS atomic per distinct key of the wave (a wave of one key --
-        // tiny frames, a homogeneous batch -- otherwise serialises 64 adds
-        // on one address)
-        uint64_t todo = __ballot(counted);
-        while (todo) {
-          const int lead = __ffsll((unsigned long long)todo) - 1;
-          const int k = __shfl(keys[r], lead, 64);
-          const uint64_t m = __ballot(counted && keys[r] == k);
-          if (lane == lead) atomicAdd((uint32_t*)&hist[k], (uint32_t)__popcll(m));
-          todo &= ~m;
-        }
-      } else if (counted) {
-        atomicAdd((uint32_t*)&hist[keys[r]], 1u);
-      }
+      if (counted) atomicAdd((uint32_t*)&hist[keys[r]], 1u);
     }
     if constexpr (!COMPACT) {
       kill_descriptors();
@@ -1286,22 +1224,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
       const int i = tid + r * kIcrcThreads;
       const bool placed = i < cnt && keys[r] >= 0;
       uint32_t pos = 0;
-      if constexpr (kHistAgg) {  // one atomic per distinct key; lanes in order within it
-        uint64_t todo = __ballot(placed);
-        while (todo) {
-          const int lead = __ffsll((unsigned long long)todo) - 1;
-          const int k = __shfl(keys[r], lead, 64);
-          const uint64_t m = __ballot(placed && keys[r] == k);
-          uint32_t base = 0;
-          if (lane == lead) base = atomicAdd((uint32_t*)&hist[k], (uint32_t)__popcll(m));
-          base = (uint32_t)__shfl((int)base, lead, 64);
-          if ((m >> lane) & 1ull)
-            pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          todo &= ~m;
-        }
-      } else if (placed) {
-        pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
-      }
+      if (placed) pos = atomicAdd((uint32_t*)&hist[keys[r]], 1u);
       if (placed) {
         perm[pos] = (uint16_t)i;
         roff[pos] = offw[r];
@@ -1431,12 +1354,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // consecutive packets: their 64 x stride bytes arrive with fully coalesced
 // 16-byte loads (issued two batches ahead, held in registers), go to the
 // wave's LDS staging slot, each lane patches its frame's masked dwords and
-// seed in place, and folds the frame from LDS as four interleaved chains:
-// chain c takes the dwords k = 4 j + c - pad (pad = 4 ns - n zero dwords in
-// front, ns = ceil(n / 4) steps), (P, T) <- Mul(128)(P ^ T ^ w_k), and the
-// packet register is R = sum_c Mul(-32 c)(chain c) -- three Horner steps with
-// Mul(-32).  The four dwords of a step are consecutive in LDS, read with
-// immediate offsets from one base (ds_read2_b32 pairs), and the joins do not
+// seed in place, and folds the frame as two interleaved chains: chain c takes
+// the dwords k = 2 j + c - pad (pad = 2 ns - n zero dwords in front, ns =
+// ceil(n / 2) steps), (P, T) <- Mul(64)(P ^ T ^ w_k), and the packet register
+// is R = Mul(-32)(chain 1) ^ chain 0 -- one Horner step.  The joins do not
 // depend on the frame length.  The batch holding the last packet reads its
 // frames straight from global memory (no 16-byte over-read past the buffer).
 //
@@ -1445,7 +1366,7 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // the prefetch.  Hence unconditional LDS writes into the slot and the masks
 // applied in LDS rather than by uniform selects in the loop.
 //
-// LDS: [0, 64 KiB) Mul(128) in the Keys8 layout (icrc_device.hpp: 8
+// LDS: [0, 64 KiB) Mul(64) in the Keys8 layout (icrc_device.hpp: 8
 // conflict-free copies in the low half of 256 rows of 256 B, one v_perm_b32
 // per address), then one staging slot of 64 x stride bytes per wave, the
 // output ring's tail, and Mul(-32) in the last 4 KiB.  The output ring
@@ -1457,41 +1378,24 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // after the slots, 8 waves were best (6-10 waves: -10 % to -2.5 %); Keys8
 // (32 KiB of tables, the ring's head in the free row halves) gained +1.8 %
 // at 8 waves.
-#ifndef RICRC_SMALL_WAVES
-#define RICRC_SMALL_WAVES 12
-#endif
-constexpr int kSmallMaxWaves = RICRC_SMALL_WAVES;
+constexpr int kSmallMaxWaves = 12;
 // Tail stealing (below): cfg5 kernel ms, 6 A/B rounds over two sessions
 // (profiles/r03q_small_tail_ab*.txt): static 0.3132-0.3161, 1/4 0.3139-0.3175,
 // 1/8 0.3115-0.3122, 1/16 0.3106-0.3148 (+0.9 % mean), 1/32 0.3122-0.3135.
-#ifndef RICRC_SMALL_TAIL_DIV
-#define RICRC_SMALL_TAIL_DIV 16
-#endif
-constexpr uint32_t kSmallTailDiv = RICRC_SMALL_TAIL_DIV;
-// Staging (A/B switch): LDS-DMA (global_load_lds_dwordx4) into the wave's slot
-// one batch ahead (default), or 16-byte loads into registers issued two
-// batches ahead and written into the slot with ds_write_b128.  cfg5 kernel ms,
-// 5 A/B rounds over two sessions (profiles/r04a, r04c cfg5_ab): register
-// staging 0.3102-0.3129, LDS-DMA 0.3058-0.3098 (-1.2 %).
-#ifndef RICRC_SMALL_DMA
-#define RICRC_SMALL_DMA 1
-#endif
-constexpr bool kSmallDma = RICRC_SMALL_DMA != 0;
-constexpr uint32_t kSmallAhead = kSmallDma ? 1u : 2u;
+constexpr uint32_t kSmallTailDiv = 16;
+// Staging: LDS-DMA (global_load_lds_dwordx4) into the wave's slot one batch
+// ahead.  cfg5 kernel ms, 5 A/B rounds over two sessions (profiles/r04a, r04c
+// cfg5_ab): 16-byte loads into registers two batches ahead, written into the
+// slot with ds_write_b128, 0.3102-0.3129; LDS-DMA 0.3058-0.3098 (-1.2 %).
+constexpr uint32_t kSmallAhead = 1;  // batches a wave's loads run ahead of its fold
 using SmallKeys = Keys8;
-// Mul(-32) for the combine: unreplicated in the last 4 KiB, or (SMALL_COMB8)
-// as 8 conflict-free copies in the high halves of the table rows, the output
-// ring then entirely after the staging slots
-#ifndef RICRC_SMALL_COMB8
-#define RICRC_SMALL_COMB8 0
-#endif
-constexpr bool kSmallComb8 = RICRC_SMALL_COMB8 != 0;
-constexpr uint32_t kSmallCombLds = 163840u - 4096u;
-constexpr uint32_t kSmallComb = kSmallComb8 ? kComb8 : kSmallCombLds;
-constexpr uint32_t kSmallEnd = kSmallComb8 ? 163840u : kSmallCombLds;  // end of the staging + ring tail
+// Mul(-32) for the combine, unreplicated in the last 4 KiB.  (8 conflict-free
+// copies in the high halves of the table rows, the output ring then entirely
+// after the staging slots: -5 %, -2 % at 10 waves.)
+constexpr uint32_t kSmallComb = 163840u - 4096u;
+constexpr uint32_t kSmallEnd = kSmallComb;  // end of the staging + ring tail
 constexpr uint32_t kSmallStage = 65536;
-constexpr uint32_t kSmallHoleWords =
-    kSmallComb8 ? 0u : 256u * (256u - Keys8::kHole) / 4u;  // ring words in the row halves
+constexpr uint32_t kSmallHoleWords = 256u * (256u - Keys8::kHole) / 4u;  // ring words in the row halves
 // LDS byte address of ring word k / ring quad i (16 B): the row halves first,
 // then the tail after the staging slots
 __device__ __forceinline__ uint32_t small_ring_word(uint32_t tail, uint32_t k) {
@@ -1502,22 +1406,15 @@ __device__ __forceinline__ uint32_t small_ring_quad(uint32_t tail, uint32_t i) {
   return i < kSmallHoleWords / 4u ? (i >> 3) * 256u + Keys8::kHole + (i & 7u) * 16u
                                   : tail + 16u * (i - kSmallHoleWords / 4u);
 }
-// Chains of the fold (A/B switch): two over Mul(64) (default), or four over
-// Mul(128).  Two need one Mul(-32) combine step instead of three and read one
-// pad dword at most: 108 lookups per 108-B frame instead of 124.  cfg5 kernel
-// ms, 6 A/B rounds over two sessions (profiles/r04p, r04q): four chains
-// 0.3050-0.3089, two 0.2980-0.3006 (-2.5 %), one (Mul(32), no combine, a
-// dependent chain of 26 lookups) 0.3257-0.3288.
-#ifndef RICRC_SMALL_CHAINS
-#define RICRC_SMALL_CHAINS 2
-#endif
-constexpr int kSmallChains = RICRC_SMALL_CHAINS;
-static_assert(kSmallChains == 2 || kSmallChains == 4, "chains");
+// Chains of the fold: two over Mul(64).  Against four over Mul(128) they need
+// one Mul(-32) combine step instead of three and read one pad dword at most:
+// 108 lookups per 108-B frame instead of 124.  cfg5 kernel ms, 6 A/B rounds
+// over two sessions (profiles/r04p, r04q): four chains 0.3050-0.3089, two
+// 0.2980-0.3006 (-2.5 %), one (Mul(32), no combine, a dependent chain of 26
+// lookups) 0.3257-0.3288.
+constexpr int kSmallChains = 2;
 constexpr int kSmallMaxSteps = (kSmallMaxStride / 4 + kSmallChains - 1) / kSmallChains;
-#ifndef RICRC_SMALL_OUTBUF
-#define RICRC_SMALL_OUTBUF 64
-#endif
-constexpr int kSmallOutRounds = RICRC_SMALL_OUTBUF;  // output ring depth in rounds (0 = off)
+constexpr int kSmallOutRounds = 64;  // output ring depth in rounds (0 = off)
 // Cache policy of the ring's flushes (out_store128).  The words written into
 // the saturating read stream cost several times their own transfer time;
 // scope-sc1 stores cut that: cfg5 4625 -> 4865 GiB/s (3 A/B rounds; nt the
@@ -1527,10 +1424,7 @@ constexpr int kSmallOutRounds = RICRC_SMALL_OUTBUF;  // output ring depth in rou
 // cheaper, but the ring cannot grow beside 8 staging slots); a 9th "writer"
 // wave draining the ring, with or without bursts aligned to a global clock,
 // 0.320-0.344.
-#ifndef RICRC_SMALL_OUT_POL
-#define RICRC_SMALL_OUT_POL 16
-#endif
-constexpr int kSmallOutPol = RICRC_SMALL_OUT_POL;
+constexpr int kSmallOutPol = 16;
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
@@ -1542,20 +1436,13 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   constexpr int CH = kSmallChains;
   const int ns = (n + CH - 1) / CH, pad = CH * ns - n;  // steps, zero dwords in front
   {
-    const uint32_t* m128 = a.tables + (CH == 4 ? 0 : kMul64Set * 1024);  // Mul(32 CH)
+    const uint32_t* m64 = a.tables + kMul64Set * 1024;  // Mul(32 CH)
     for (int i = tid; i < 2048; i += (int)blockDim.x) {  // 8 copies of 1024 words, 2 quads
       const int w = i >> 1, h = i & 1;  // w = t * 256 + e
-      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m128[w]);
+      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m64[w]);
     }
     const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
-    if constexpr (kSmallComb8) {
-      for (int i = tid; i < 2048; i += (int)blockDim.x) {
-        const int w = i >> 1, h = i & 1;
-        lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128), cm32[w]);
-      }
-    } else {
-      for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallCombLds + 4u * i, cm32[i]);
-    }
+    for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallComb + 4u * i, cm32[i]);
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
@@ -1659,28 +1546,25 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       a.claims ? a.claims + (size_t)(a.epoch % kClaimSlots) * kMaxClaimBlocks : nullptr;
   if (claims && tid == 0) atomicExch(&claims[blockIdx.x], (unsigned long long)a.epoch << 32);
   uint32_t lim = bs_end > 0 ? bs_end - 1u : 0u;  // prefetch clamp (no clamp while claiming)
-  auto load = [&](uint32_t b, u32x4* Rg) __attribute__((always_inline)) {  // unconditional: clamped chunk index
+  auto load = [&](uint32_t b) __attribute__((always_inline)) {  // unconditional: clamped batch index
     const uint8_t* base = a.frames + (uint64_t)min(b, lim) * 64u * S;
-    if constexpr (kSmallDma) {
-      // LDS-DMA straight into the wave's slot: chunk lane + 64 t of the
-      // batch lands at stage + 1024 t + 16 lane, the register path's layout;
-      // lanes past the batch's last chunk stay idle (the slot holds exactly
-      // the batch)
+    // LDS-DMA straight into the wave's slot: chunk lane + 64 t of the batch
+    // lands at stage + 1024 t + 16 lane; lanes past the batch's last chunk
+    // stay idle (the slot holds exactly the batch)
 #pragma unroll
-      for (int t = 0; t < C; ++t)
-        if ((uint32_t)(lane + 64 * t) < nchunk)
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void*)(base + 16u * (uint32_t)(lane + 64 * t)),
-              (__attribute__((address_space(3))) void*)(uintptr_t)(stage + 1024u * (uint32_t)t), 16, 0, 2);
-    } else {
-#pragma unroll
-      for (int t = 0; t < C; ++t) Rg[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1));
-    }
+    for (int t = 0; t < C; ++t)
+      if ((uint32_t)(lane + 64 * t) < nchunk)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(base + 16u * (uint32_t)(lane + 64 * t)),
+            (__attribute__((address_space(3))) void*)(uintptr_t)(stage + 1024u * (uint32_t)t), 16, 0, 2);
   };
-  // LDS-DMA staging (A/B switch): the slot's batch has landed; its frames are
-  // patched in LDS and read into registers, the slot is refilled with the
-  // next batch (in flight during the fold), the fold runs from registers
-  auto dma_fold = [&](uint32_t b, uint32_t bnext, bool live, bool to_ring) __attribute__((always_inline)) {
+  // One batch: the slot's batch has landed; its frames are patched in LDS and
+  // read into registers, the slot is refilled with the next batch (in flight
+  // during the fold, its loads at raised wave priority), the fold runs from
+  // registers.  live: the batch is the wave's (its words are emitted);
+  // to_ring: its words go to the output ring (when there is one).
+  auto stage_and_fold = [&](uint32_t b, uint32_t bnext, bool live = true,
+                            bool to_ring = true) __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch is in the slot
     __asm__ __volatile__("" ::: "memory");
     const uint32_t pb = stage + (uint32_t)lane * S;
@@ -1703,7 +1587,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read
       __asm__ __volatile__("" ::: "memory");
       body_prio_hi();
-      load(bnext, nullptr);
+      load(bnext);
       body_prio_lo();
       R = fold4([&](int, int kp) { return D[kp]; });
     } else {
@@ -1711,61 +1595,21 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       __asm__ __volatile__("" ::: "memory");
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __asm__ __volatile__("" ::: "memory");
-      load(bnext, nullptr);
+      load(bnext);
     }
     emit(b * 64u + (uint32_t)lane, live, st, R, trailer, kRing && to_ring);
     __asm__ __volatile__("" ::: "memory");
   };
-  auto stage_and_fold = [&](uint32_t b, u32x4* Rg, uint32_t bnext, bool live = true,
-                            bool to_ring = true) __attribute__((always_inline)) {  // (to the ring when there is one)
-    if constexpr (kSmallDma) {
-      dma_fold(b, bnext, live, to_ring);
-      return;
-    }
-    // staging and the prefetch go out at raised wave priority: cfg5 +2.5 to
-    // +12 % (4326 -> 4437-4855 GiB/s, 6 A/B rounds on two boxes; priority 1-2
-    // +2-3 %; raising it for the output stores as well measured 12 % slower,
-    // for the fold at 1-2 +0.3 %, for the staging too +0.5 %, kept)
-    body_prio_hi();
-#pragma unroll
-    for (int t = 0; t < C; ++t)  // chunks past the batch hold a copy of its last one
-      *(lds_u32x4*)(uintptr_t)(stage + 16u * min((uint32_t)(lane + 64 * t), nchunk - 1)) = Rg[t];
-    __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
-    load(bnext, Rg);  // the registers are free again: prefetch the next batch
-    body_prio_lo();
-    const uint32_t pb = stage + (uint32_t)lane * S;
-    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
-    int ihl;
-    uint32_t st = check(d0, d2, ihl);
-    uint32_t R;
-    if (__all((st & kPktFatal) == 0 && ihl == 5)) {
-      // IHL 5 everywhere: patch the masked dwords and the seed in place
-      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
-      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
-      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
-      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
-      __asm__ __volatile__("" ::: "memory");
-      const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
-      R = fold4([&](int, int kp) { return lds_rd(pz + 4u * (uint32_t)kp); });
-    } else {
-      R = small_fold_masked<false, SmallKeys, kSmallComb, CH>(nullptr, pb, ihl, n);
-    }
-    emit(b * 64u + (uint32_t)lane, live, st, R, VERIFY ? lds_rd(pb + 4u * n) : 0u, kRing && to_ring);
-    __asm__ __volatile__("" ::: "memory");
-  };
 
-  // staged batches [b0 + wave, bs_end) step nw; each batch's loads are
-  // issued two batches ahead (buffers X, Y), right after the batch that used
-  // the buffer is staged (a third buffer measured no faster)
+  // staged batches [b0 + wave, bs_end) step nw, each batch's loads issued one
+  // batch ahead (kSmallAhead), two rounds per loop iteration
   if (kRing && rounds_cap > 0 && b0 < bs_end) {  // (uniform)
     // rounds: round r is batch b0 + r nw + wave of every wave (waves past
     // bs_end recompute a clamped batch and emit nothing); every rounds_cap
     // rounds the ring goes out.  LDS-only waits at the barriers: the
     // prefetched loads stay in flight across them.
     const uint32_t nrounds = (bs_end - b0 + nw - 1) / nw;
-    u32x4 X[C], Y[C];
-    load(b0 + (uint32_t)wave, X);
-    if constexpr (!kSmallDma) load(b0 + (uint32_t)wave + nw, Y);
+    load(b0 + (uint32_t)wave);
     ring_base = b0 * 64u;
     uint32_t in_ring = 0;
     auto flush = [&]() {
@@ -1790,11 +1634,11 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     };
     for (uint32_t r = 0; r < nrounds; r += 2) {
       uint32_t b = b0 + r * nw + (uint32_t)wave;
-      stage_and_fold(b, X, b + kSmallAhead * nw, b < bs_end);
+      stage_and_fold(b, b + kSmallAhead * nw, b < bs_end);
       if (++in_ring == rounds_cap) flush();
       if (r + 1 < nrounds) {
         b += nw;
-        stage_and_fold(b, Y, b + kSmallAhead * nw, b < bs_end);
+        stage_and_fold(b, b + kSmallAhead * nw, b < bs_end);
         if (++in_ring == rounds_cap) flush();
       }
     }
@@ -1802,16 +1646,14 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   } else if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
     const uint32_t first = b0 + (uint32_t)wave;
     const int cnt = first < bs_end ? (int)((bs_end - first + nw - 1) / nw) : 0;
-    u32x4 X[C], Y[C];
-    load(first, X);
-    if constexpr (!kSmallDma) load(first + nw, Y);
+    load(first);
     uint32_t b = first;
     int i = 0;
     for (; i + 1 < cnt; i += 2, b += 2 * nw) {
-      stage_and_fold(b, X, b + kSmallAhead * nw);
-      stage_and_fold(b + nw, Y, b + nw + kSmallAhead * nw);
+      stage_and_fold(b, b + kSmallAhead * nw);
+      stage_and_fold(b + nw, b + nw + kSmallAhead * nw);
     }
-    if (i < cnt) stage_and_fold(b, X, b + kSmallAhead * nw);
+    if (i < cnt) stage_and_fold(b, b + kSmallAhead * nw);
   }
   if (claims) {  // own tail, then up to kMaxVictims other workgroups' tails
     lim = 0xFFFFFFFFu;
@@ -1831,17 +1673,16 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     };
     uint32_t cur = claim();
     if (cur != ~0u) {
-      u32x4 X[C];
-      load(cur, X);
+      load(cur);
       for (;;) {  // the next claim's loads go out while this batch folds
         const uint32_t nxt = claim();
-        stage_and_fold(cur, X, nxt == ~0u ? cur : nxt, true, false);
+        stage_and_fold(cur, nxt == ~0u ? cur : nxt, true, false);
         if (nxt == ~0u) break;
         cur = nxt;
       }
     }
   }
-  if constexpr (kSmallDma) __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA outlives its slot's use
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA outlives its slot's use
   // the last batch, straight from global memory (one wave of the owning block)
   if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % nw) {
     const uint32_t pkt = last * 64u + (uint32_t)lane;
@@ -1906,10 +1747,7 @@ __global__ void __launch_bounds__(kStreamThreads) stream_read_kernel(const u32x4
 // every path through the loop reaches one of the two, so the grid always
 // drains; the host relaunches it on the next call.
 // Polls of the request slot in flight at once (2 or 4; A/B switch).
-#ifndef RICRC_SVC_POLLS
-#define RICRC_SVC_POLLS 2
-#endif
-constexpr int kSvcPolls = RICRC_SVC_POLLS;
+constexpr int kSvcPolls = 2;
 constexpr int kSvcThreads = 512;  // all stage the tables; wave 0 serves, waves 1-7 help with bursts
 constexpr int kSvcWaves = kSvcThreads / 64;
 // LDS of the service (round 3): Mul(8192) for single frames (G = 64) and
@@ -2280,7 +2118,7 @@ typedef void (*kernel_fn)(IcrcArgs);
 
 template <int LOG2G>
 kernel_fn pick(bool ragged, bool verify, bool compact) {
-  if (ragged && LOG2G == 3 && RICRC_RAGGED_MIXED) {
+  if (ragged && ragged_has_compact(LOG2G)) {  // the mixed-width kernel
     if (compact) return verify ? icrc_ragged_mixed_kernel<true, true> : icrc_ragged_mixed_kernel<false, true>;
     return verify ? icrc_ragged_mixed_kernel<true, false> : icrc_ragged_mixed_kernel<false, false>;
   }
@@ -2307,7 +2145,7 @@ size_t lds_bytes(int log2g, bool ragged) {
     case 0: return RaggedLds<0>::kBytes;
     case 1: return RaggedLds<1>::kBytes;
     case 2: return RaggedLds<2>::kBytes;
-    case 3: return RICRC_RAGGED_MIXED ? kMixedLdsBytes : RaggedLds<3>::kBytes;
+    case 3: return kMixedLdsBytes;
     case 4: return RaggedLds<4>::kBytes;
     case 5: return RaggedLds<5>::kBytes;
     default: return RaggedLds<6>::kBytes;
@@ -2381,7 +2219,7 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
   const uint64_t nsets = (a.n + ppw - 1) / ppw;
   const int waves = ragged ? kIcrcWaves : kStridedWaves;
   uint64_t blocks = (nsets + waves - 1) / waves;
-  const uint64_t cap = (uint64_t)num_cus * (ragged ? RICRC_RAGGED_BLOCKS_PER_CU : 1);
+  const uint64_t cap = (uint64_t)num_cus;  // one workgroup per CU (the LDS holds one)
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * waves), lds_bytes(log2g, ragged), stream, a);
@@ -2395,11 +2233,7 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   // strides (cfg5, 108 B: 432 chunks): with C = 8 every lane's 8th load and
   // LDS write were copies of the batch's last chunk (64 lanes writing one
   // 16-byte LDS address)
-#ifndef RICRC_SMALL_NO_C7
   const int C = a.stride <= 64 ? 4 : a.stride <= 112 ? 7 : 8;
-#else
-  const int C = a.stride <= 64 ? 4 : 8;
-#endif
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
   kernel_fn k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;

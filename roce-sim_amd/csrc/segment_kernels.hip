@@ -47,28 +47,18 @@ __device__ __forceinline__ u32x4 ldmr(const uint8_t* p) {
   return *(const u32x4_u*)p;
 }
 
-#ifndef RICRC_SEG_UNROLL
-#define RICRC_SEG_UNROLL 4
-#endif
-#ifndef RICRC_SEG_THREADS
-#define RICRC_SEG_THREADS 512  // 8 waves x ~200 VGPRs: no spills (16 waves spill ~20 VGPRs)
-#endif
-constexpr int kSegUnroll = RICRC_SEG_UNROLL;  // body iterations (16-byte MR loads per lane) in flight
-#ifndef RICRC_SEG_TAIL_DIV
-#define RICRC_SEG_TAIL_DIV 4
-#endif
+constexpr int kSegUnroll = 4;  // body iterations (16-byte MR loads per lane) in flight
 // last 1/kSegTailDiv of a range claimed dynamically: seg kernel ms (3 A/B
 // rounds, profiles/r03q_seg_tail_ab.txt) static 1.692-1.723, 1/4
 // 1.660-1.691 (+1.8 %), 1/8 1.661-1.701, 1/16 1.692-1.693
-constexpr uint32_t kSegTailDiv = RICRC_SEG_TAIL_DIV;
+constexpr uint32_t kSegTailDiv = 4;
 constexpr uint32_t kSegMaxVictims = 4;
-constexpr int kSegThreads = RICRC_SEG_THREADS;  // one workgroup per CU (the tables fill the LDS)
+// one workgroup per CU (the tables fill the LDS); 8 waves x ~200 VGPRs: no
+// spills (16 waves spill ~20 VGPRs)
+constexpr int kSegThreads = 512;
 constexpr int kSegWaves = kSegThreads / 64;
 // Cache policy of the frame stores (stg128 in icrc_device.hpp; 2 = nt).
-#ifndef RICRC_SEG_STORE_POL
-#define RICRC_SEG_STORE_POL 2
-#endif
-constexpr int kSegStorePol = RICRC_SEG_STORE_POL;
+constexpr int kSegStorePol = 2;
 constexpr uint32_t kRocePort = 4791;   // src/roce_enum.py ROCE_PORT
 constexpr uint32_t kAckValue = 31;     // CREDIT_CNT_INVALID, src/roce_enum.py:8
 // AETH.code (src/roce.py:267): ACK 0, RNR 1, NAK 3
