@@ -45,6 +45,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace ricrc {
 
 namespace {
@@ -1426,15 +1428,23 @@ constexpr int kSmallOutRounds = 64;  // output ring depth in rounds (0 = off)
 // 0.320-0.344.
 constexpr int kSmallOutPol = 16;
 
-template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
+// NS > 0: the fold's step count ceil(n / 2) fixed at compile time (packed
+// batches, stride == frame length, launch_icrc_small): every per-dword read
+// and step of the unrolled fold is unconditional.  NS = 0 takes it from the
+// frame length at run time, one uniform branch per dword -- with 92 SGPRs
+// spilled into VGPR lanes on top (cfg5 kernel: 6570 instructions, 4308 with
+// NS = 13).
+template <int C, int NS, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
   const uint32_t S = (uint32_t)a.stride, L = a.len;
   announce_batch(a.busy);
   const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
-  const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
   constexpr int CH = kSmallChains;
-  const int ns = (n + CH - 1) / CH, pad = CH * ns - n;  // steps, zero dwords in front
+  const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
+  // steps, zero dwords in front (0 or 1); with NS the launcher checked that
+  // the frames are not `dead` and that ceil(n / CH) == NS
+  const int ns = NS > 0 ? NS : (n + CH - 1) / CH, pad = CH * ns - n;
   {
     const uint32_t* m64 = a.tables + kMul64Set * 1024;  // Mul(32 CH)
     for (int i = tid; i < 2048; i += (int)blockDim.x) {  // 8 copies of 1024 words, 2 quads
@@ -1550,52 +1560,63 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* base = a.frames + (uint64_t)min(b, lim) * 64u * S;
     // LDS-DMA straight into the wave's slot: chunk lane + 64 t of the batch
     // lands at stage + 1024 t + 16 lane; lanes past the batch's last chunk
-    // stay idle (the slot holds exactly the batch)
+    // stay idle (the slot holds exactly the batch; with NS, frames of at
+    // least 8 NS bytes, the first 32 NS / 64 loads are whole without a test)
 #pragma unroll
     for (int t = 0; t < C; ++t)
-      if ((uint32_t)(lane + 64 * t) < nchunk)
+      if ((NS > 0 && 64 * t + 64 <= 32 * NS) || (uint32_t)(lane + 64 * t) < nchunk)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(base + 16u * (uint32_t)(lane + 64 * t)),
             (__attribute__((address_space(3))) void*)(uintptr_t)(stage + 1024u * (uint32_t)t), 16, 0, 2);
   };
-  // One batch: the slot's batch has landed; its frames are patched in LDS and
-  // read into registers, the slot is refilled with the next batch (in flight
-  // during the fold, its loads at raised wave priority), the fold runs from
-  // registers.  live: the batch is the wave's (its words are emitted);
-  // to_ring: its words go to the output ring (when there is one).
+  // One batch: the slot's batch has landed; the wave reads its frames into
+  // registers and at once refills the slot with the next batch (in flight
+  // during the fold, its loads at raised wave priority), then checks the
+  // headers, applies the masks and the seed in registers and folds.  (Round
+  // 4 patched the masked dwords in LDS first: two LDS round trips before the
+  // next batch's loads could go out.)  live: the batch is the wave's (its
+  // words are emitted); to_ring: its words go to the output ring (when there
+  // is one).
   auto stage_and_fold = [&](uint32_t b, uint32_t bnext, bool live = true,
                             bool to_ring = true) __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch is in the slot
     __asm__ __volatile__("" ::: "memory");
     const uint32_t pb = stage + (uint32_t)lane * S;
-    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+    const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
+    uint32_t D[CH * kSmallMaxSteps];
+#pragma unroll
+    for (int kp = 0; kp < CH * kSmallMaxSteps; ++kp) D[kp] = kp < CH * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
     const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * n) : 0u;
+    __asm__ __volatile__("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read
+    __asm__ __volatile__("" ::: "memory");
+    body_prio_hi();
+    load(bnext);
+    body_prio_lo();
+    // (pad is 0 or 1 and uniform: dword k is D[k] or D[k + 1])
+    const bool p1 = pad != 0;
+    const uint32_t d0 = p1 ? D[1] : D[0], d2 = p1 ? D[3] : D[2];
     int ihl;
     uint32_t st = check(d0, d2, ihl);
     uint32_t R;
     if (__all((st & kPktFatal) == 0 && ihl == 5)) {
-      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
-      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
-      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
-      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
-      __asm__ __volatile__("" ::: "memory");
-      const uint32_t pz = pb - 4u * (uint32_t)pad;
-      uint32_t D[CH * kSmallMaxSteps];
-#pragma unroll
-      for (int kp = 0; kp < CH * kSmallMaxSteps; ++kp) D[kp] = kp < CH * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
-      __asm__ __volatile__("" ::: "memory");
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read
-      __asm__ __volatile__("" ::: "memory");
-      body_prio_hi();
-      load(bnext);
-      body_prio_lo();
+      // IHL 5 everywhere: the masked dwords 0, 2, 6, 8 and the seed
+      if (p1) {
+        D[1] = (D[1] | 0x0000FF00u) ^ kSeedRegister;
+        D[3] |= 0xFFFF00FFu;
+        D[7] |= 0xFFFF0000u;
+        D[9] |= 0x000000FFu;
+      } else {
+        D[0] = (D[0] | 0x0000FF00u) ^ kSeedRegister;
+        D[2] |= 0xFFFF00FFu;
+        D[6] |= 0xFFFF0000u;
+        D[8] |= 0x000000FFu;
+      }
       R = fold4([&](int, int kp) { return D[kp]; });
-    } else {
-      R = small_fold_masked<false, SmallKeys, kSmallComb, CH>(nullptr, pb, ihl, n);
-      __asm__ __volatile__("" ::: "memory");
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __asm__ __volatile__("" ::: "memory");
-      load(bnext);
+    } else {  // per-dword masks (IPv4 options; malformed frames), from HBM
+      // (out of line; the slot already holds the next batch)
+      const uint8_t* f = a.frames + (uint64_t)(b * 64u + (uint32_t)lane) * S;
+      R = small_fold_masked<true, SmallKeys, kSmallComb, CH>(live ? f : a.frames, 0u, ihl, n);
     }
     emit(b * 64u + (uint32_t)lane, live, st, R, trailer, kRing && to_ring);
     __asm__ __volatile__("" ::: "memory");
@@ -2155,10 +2176,10 @@ size_t lds_bytes(int log2g, bool ragged) {
 template <int C, bool V>
 kernel_fn pick_small(int outs) {
   switch (outs) {
-    case 0: return icrc_small_kernel<C, V, 0>;
-    case 1: return icrc_small_kernel<C, V, 1>;
-    case 2: return icrc_small_kernel<C, V, 2>;
-    default: return icrc_small_kernel<C, V, 3>;
+    case 0: return icrc_small_kernel<C, 0, V, 0>;
+    case 1: return icrc_small_kernel<C, 0, V, 1>;
+    case 2: return icrc_small_kernel<C, 0, V, 2>;
+    default: return icrc_small_kernel<C, 0, V, 3>;
   }
 }
 
@@ -2166,6 +2187,34 @@ kernel_fn select_small(int C, bool verify, int outs) {
   if (C == 4) return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
   if (C == 7) return verify ? pick_small<7, true>(outs) : pick_small<7, false>(outs);
   return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
+}
+
+// Exact-step instantiations of packed batches (stride == frame length L):
+// C = 4 for 44-64-B frames (NS 5-8), 7 for 68-112 B (NS 8-14), 8 for
+// 116-128 B (NS 14-16), for the device-resident forms -- compute with ICRC
+// words only, verify with verdicts (with or without the words).  Other output
+// sets, and strides wider than the frames, take NS = 0.
+template <int C, int NS>
+kernel_fn pick_small_exact(bool verify, int outs) {
+  if (!verify && outs == 1) return icrc_small_kernel<C, NS, false, 1>;
+  if (verify && outs == 0) return icrc_small_kernel<C, NS, true, 0>;
+  if (verify && outs == 1) return icrc_small_kernel<C, NS, true, 1>;
+  return nullptr;
+}
+
+template <int C, int NS0, int... K>
+kernel_fn select_small_exact_in(int ns, bool verify, int outs, std::integer_sequence<int, K...>) {
+  kernel_fn k = nullptr;
+  ((ns == NS0 + K ? (k = pick_small_exact<C, NS0 + K>(verify, outs)) : k), ...);
+  return k;
+}
+
+// nullptr: no exact instantiation for this (C, step count, output set)
+kernel_fn select_small_exact(int C, int ns, bool verify, int outs) {
+  if (C == 4) return select_small_exact_in<4, 5>(ns, verify, outs, std::make_integer_sequence<int, 4>{});
+  if (C == 7) return select_small_exact_in<7, 8>(ns, verify, outs, std::make_integer_sequence<int, 7>{});
+  if (C == 8) return select_small_exact_in<8, 14>(ns, verify, outs, std::make_integer_sequence<int, 3>{});
+  return nullptr;
 }
 
 }  // namespace
@@ -2200,6 +2249,14 @@ hipError_t prepare_kernels() {
         hipError_t e = set_dynamic_lds((const void*)select_small(c, v, o), 163840);
         if (e != hipSuccess) return e;
       }
+  for (int c : {4, 7, 8})
+    for (int ns = 1; ns <= kSmallMaxSteps; ++ns)
+      for (int v = 0; v < 2; ++v)
+        for (int o = 0; o < 2; ++o)
+          if (kernel_fn k = select_small_exact(c, ns, v, o)) {
+          hipError_t e = set_dynamic_lds((const void*)k, 163840);
+          if (e != hipSuccess) return e;
+        }
   hipError_t e = set_dynamic_lds((const void*)icrc_service_kernel, (int)kSvcLds);
   if (e != hipSuccess) return e;
   return prepare_segment_kernels();
@@ -2235,7 +2292,11 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   // 16-byte LDS address)
   const int C = a.stride <= 64 ? 4 : a.stride <= 112 ? 7 : 8;
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
-  kernel_fn k = select_small(C, verify, outs);
+  kernel_fn k = nullptr;
+  const uint32_t L = a.len;
+  if (L == a.stride && L >= 44 && (L & 3u) == 0)  // packed, and not `dead` (L <= stride <= 128)
+    k = select_small_exact(C, (int)(((L - 4) / 4 + kSmallChains - 1) / kSmallChains), verify, outs);
+  if (!k) k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;
   uint32_t nw = min((uint32_t)kSmallMaxWaves, (kSmallEnd - kSmallStage) / slot);
   if (nw > 2 && (nw & 1u)) --nw;  // even: every SIMD the same number of waves

@@ -98,3 +98,67 @@ def test_small_kernel_verify(engine, n):
     want[flip] = False
     np.testing.assert_array_equal(okh, want)
     assert (sth[flip] & PKT_ICRC_MISMATCH).all() and not sth[want].any()
+
+
+def _dev_strided(engine, buf, L, n, verify):
+    """Device-resident packed batch (stride == L): compute with ICRC words only
+    (the exact-step kernel of the compute form), or verify with verdicts only
+    and with verdicts + words (its two verify forms)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(buf).to(dev)
+    if not verify:
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        engine.compute_strided_dev(d, L, L, n, out)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint32)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.verify_strided_dev(d, L, L, n, ok)
+    ok2 = torch.zeros(n, dtype=torch.uint8, device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    engine.verify_strided_dev(d, L, L, n, ok2, out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ok.cpu().numpy(), ok2.cpu().numpy())
+    return ok.cpu().numpy().astype(bool), out.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("L", list(range(44, 129, 4)))
+def test_exact_step_kernels_every_packed_length(engine, L):
+    """Packed batches (stride == frame length) run kernels whose fold step
+    count is a compile-time constant (icrc_small_kernel<C, NS>, NS =
+    ceil((L - 4) / 8)): every length 44..128 B, batch counts across the
+    64-packet batch, ring and last-batch boundaries, compute and both verify
+    forms, against the oracle."""
+    rng = np.random.default_rng(L)
+    for n in (1, 63, 64, 65, 4099, 70001):
+        buf = _strided(n, L, L, rng) if n <= 4099 else np.tile(_strided(4099, L, L, rng),
+                                                               n // 4099 + 1)[:n * L].copy()
+        want, _ = oracle_batch(buf, stride=L, length=L, n=n)
+        got = _dev_strided(engine, buf, L, n, verify=False)
+        np.testing.assert_array_equal(got, want, err_msg=f"L {L} n {n}")
+        frames = buf.reshape(n, L)
+        frames[:, L - 4:] = want.astype("<u4").view(np.uint8).reshape(n, 4)
+        flip = np.arange(3, n, 37)
+        frames[flip, L - 8] ^= 0x01  # the last covered dword: must fail
+        ok, words = _dev_strided(engine, buf, L, n, verify=True)
+        expect = np.ones(n, bool)
+        expect[flip] = False
+        np.testing.assert_array_equal(ok, expect, err_msg=f"L {L} n {n}")
+        frames[flip, L - 8] ^= 0x01
+        np.testing.assert_array_equal(words, want, err_msg=f"L {L} n {n}")
+
+
+@pytest.mark.parametrize("L", [48, 68, 108, 128])
+def test_exact_step_kernels_options_and_malformed(engine, L):
+    """The exact-step kernels' batches holding IPv4-option or malformed frames
+    fold from HBM through the per-dword masks (the slot already holds the next
+    batch): ICRC words against the oracle, malformed frames 0."""
+    n = 64 * 50 + 9
+    rng = np.random.default_rng(L + 1)
+    buf = _strided(n, L, L, rng, ihl6_every=29, bad_every=31)
+    want = np.array([o.icrc_of_frame(bytes(buf[i * L:(i + 1) * L])) or 0 for i in range(n)],
+                    np.uint32)
+    got = _dev_strided(engine, buf, L, n, verify=False)
+    np.testing.assert_array_equal(got, want)
+    bad = np.array([i % 31 == 5 for i in range(n)])
+    assert (got[bad] == 0).all()
