@@ -1348,6 +1348,290 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 }
 
 // ---------------------------------------------------------------------------
+// The ragged COMPACT variant as a kernel of its own (round 5): packed runs of
+// small frames -- the responder's ACK / NAK / atomic-ack stream
+// (src/roce_rq.py:767-853) -- streamed group by group, with no windows, no
+// window barriers and no sort.
+//
+// A wave takes 64-packet groups of its workgroup's contiguous range
+// (round-robin over the workgroup's waves).  Per group: the lanes' 12-byte
+// descriptors, then the compact test of phase 0 (every live frame 44-128 B,
+// dword-aligned, in order without overlap, inside 4 KiB from the first
+// frame's 16-byte line); a compact group's span arrives with four coalesced
+// 16-byte loads per lane, goes to the wave's LDS slot, and each lane patches
+// and folds its frame there (four Mul(128) chains, three Mul(-32) steps, as
+// the window kernel's phase 0).  The pipeline per wave, two register sets
+// ping-ponging: while group i folds, the spans of groups i+1 and i+2 and the
+// descriptors of group i+3 are in flight -- eight KiB per wave, 128 KiB per
+// CU, against phase 0's one span per wave and a descriptor round trip plus
+// three barriers per 8192-packet window.  A group that fails the test
+// (frames out of order, overlapping, larger, unaligned) is folded in place
+// by G = 8 lane groups, eight packets at a time, out of line
+// (compact_fallback_group).
+constexpr int kCompactWaves = 12;
+constexpr int kCompactThreads = 64 * kCompactWaves;
+constexpr uint32_t kCompactSlots = kMixedLut + 256u;  // a kCompactSpan slot per wave
+static_assert(kCompactSlots + kCompactWaves * kCompactSpan <= 163840u, "compact kernel LDS");
+
+// One group of a wave after its test.  Per lane: descriptor, offset in the
+// span; uniform: the span's start (from the 16-byte line below frames) and
+// length, 0 when the group is not compact.
+struct CGroup {
+  uint32_t L;
+  uint64_t off;
+  uint32_t rel;
+  uint64_t b16;
+  uint32_t span;
+};
+
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
+
+// The test of group g (packets 64 g ..), from the lane's descriptor.
+__device__ __forceinline__ CGroup compact_test(const IcrcArgs& a, uint32_t g, uint32_t L, uint64_t off,
+                                               int lane) {
+  CGroup c;
+  c.L = L;
+  c.off = off;
+  c.rel = 0;
+  c.b16 = 0;
+  c.span = 0;
+  const uint32_t p0 = g * 64u;
+  if (p0 >= a.n) return c;  // (uniform) past the batch
+  const int nlive = (int)min(64u, a.n - p0);
+  const bool live = lane < nlive;
+  const uint64_t addr = a.frames_lo4 + off;  // (from the line below frames)
+  const uint64_t b16 = readfirstlane64(addr) & ~15ull;
+  const uint64_t rel64 = addr - b16;
+  const uint32_t rel = rel64 < kCompactSpan ? (uint32_t)rel64 : 0xFFFF0000u;
+  const uint32_t end = rel + L;
+  // the left neighbour's end: one DPP wave shift (lane 0 gets 0)
+  const uint32_t prev_end = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)end, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+  const bool ok = !live || (L >= 44 && L <= kCompactMaxLen && (L & 3u) == 0 && (rel & 3u) == 0 &&
+                            end <= kCompactSpan && rel >= prev_end);
+  if (__all(ok)) {
+    c.rel = rel;
+    c.b16 = b16;
+    // in order without overlap: the last live frame ends the span
+    c.span = (uint32_t)__builtin_amdgcn_readlane((int)end, nlive - 1);
+  }
+  return c;
+}
+
+// A group that is not compact: eight sets of eight packets, G = 8 lanes per
+// packet (the window kernel's long-frame path, unsorted), Mul(1024) from the
+// table rows' low halves.  Out of line: the compact loop's registers stay its
+// own.
+template <bool VERIFY>
+__device__ __noinline__ void compact_fallback_group(const uint8_t* frames, uint32_t n, uint32_t* icrc_out,
+                                                    uint8_t* status_out, uint8_t* ok_out, uint32_t g,
+                                                    uint32_t L, uint64_t off) {
+  IcrcArgs a{};
+  a.frames = frames;
+  a.n = n;
+  a.icrc_out = icrc_out;
+  a.status_out = status_out;
+  a.ok_out = ok_out;
+  const int lane = __lane_id();
+  const int gl = lane & 7, grp = lane >> 3;
+  const MixedKeysL kk = MixedKeysL::make(lane);
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const int src = 8 * k + grp;
+    const uint32_t pkt = g * 64u + (uint32_t)src;
+    const bool live = pkt < n;
+    const uint32_t Ls = (uint32_t)__shfl((int)L, src, 64);
+    const uint64_t os = (uint64_t)(uint32_t)__shfl((int)(uint32_t)off, src, 64) |
+                        ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), src, 64) << 32);
+    const Pkt p = describe<32>(frames, pkt, live, live ? os : 0, live ? Ls : 0);
+    Batch<kUnroll> b = issue_packet<3, VERIFY>(p, gl);
+    finish_packet<3, VERIFY, MixedKeysL, kMixedLut>(a, p, b, gl, grp * 8, kk, OutBuf{0, 0});
+  }
+}
+
+template <bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
+__global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcArgs a) {
+  const int tid = threadIdx.x;
+  announce_batch(a.busy);
+  // the window kernel's tables in phase 0: Mul(1024) in the rows' low halves
+  // with its combine sets and fix-up LUT (fallback groups), Mul(128) in the
+  // high halves (compact groups)
+  const uint32_t probe = blockIdx.x == 0 ? a.lens[min((uint32_t)tid, a.n - 1u)] : 0xFFFFFFFFu;
+  stage_tables<3, kCompactThreads, MixedKeysL>(a.tables, tid);
+  MixedKeysS::template stage<kCompactThreads>(a.tables + 0 * 1024, tid);
+  if (a.tiny_hint && blockIdx.x == 0) {  // (uniform) the AUTO hint, as the window kernel stores it
+    if ((tid & 63) == 0)
+      lds_wr(kCompactSlots + 4u * (uint32_t)(tid >> 6), __any(probe <= kCompactMaxLen) ? 1u : 0u);
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t any = 0;
+#pragma unroll
+      for (int w = 0; w < kCompactWaves; ++w) any |= lds_rd(kCompactSlots + 4u * (uint32_t)w);
+      __hip_atomic_store(a.tiny_hint, any ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const MixedKeysS kk = MixedKeysS::make(lane);
+  constexpr uint32_t kComb = MixedKeysS::kComb;  // Mul(-32)
+  const uint32_t slot = kCompactSlots + (uint32_t)wave * kCompactSpan;
+  const uint32_t ngroups = (a.n + 63u) / 64u;
+  const uint32_t per_block = (ngroups + gridDim.x - 1) / gridDim.x;
+  const uint32_t g0 = blockIdx.x * per_block;
+  const uint32_t g1 = min(ngroups, g0 + per_block);
+  // this wave's groups: g0 + wave + kCompactWaves i, i < cnt
+  const uint32_t first = g0 + (uint32_t)wave;
+  const int cnt = first < g1 ? (int)((g1 - first + kCompactWaves - 1) / kCompactWaves) : 0;
+  if (cnt == 0) return;
+  auto group = [&](int i) { return first + (uint32_t)i * kCompactWaves; };
+  // descriptors of the wave's group i (clamped: unconditional loads)
+  auto load_desc = [&](int i, uint32_t& L, uint64_t& off) __attribute__((always_inline)) {
+    const uint32_t gi = group(min(i, cnt - 1));
+    const uint32_t p = min(gi * 64u + (uint32_t)lane, a.n - 1u);
+    L = a.lens[p];
+    off = a.offsets[p];
+  };
+  // a compact group's span chunks (unconditional, clamped); a group that is
+  // not compact loads 16 bytes of the table image (always mapped, L2-hot)
+  auto issue = [&](const CGroup& c, u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
+    const bool cp = c.span != 0;
+    const uint8_t* base = cp ? a.frames + (c.b16 - a.frames_lo4) : (const uint8_t*)a.tables;
+    const uint32_t last = cp ? (c.span + 15u) / 16u - 1u : 0u;
+#pragma unroll
+    for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
+  };
+  // group i: patch, fold and emit from the slot (compact), or the fallback
+  auto run = [&](int i, const CGroup& c) __attribute__((always_inline)) {
+    const uint32_t gi = group(i);
+    if (c.span == 0) {  // (uniform)
+      compact_fallback_group<VERIFY>(a.frames, a.n, (OUTS & 1) ? a.icrc_out : nullptr,
+                                     (OUTS & 2) ? a.status_out : nullptr, a.ok_out, gi, c.L, c.off);
+      return;
+    }
+    // (an opaque lane id: the compiler otherwise hoists the output addresses
+    // of both unrolled groups)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint32_t pkt = gi * 64u + (uint32_t)ln;
+    const bool live = pkt < a.n;
+    const uint32_t L = c.L;  // (dead lanes repeat the last live frame)
+    const uint32_t pb = slot + c.rel;
+    const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the test checked every lane)
+    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+    const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
+    uint32_t st = 0;
+    const int ihl = (int)(d0 & 0xFu);
+    if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
+      st |= kPktNotIpv4;
+    else if (((d2 >> 8) & 0xFFu) != 17u)
+      st |= kPktNotUdp;
+    else if (L < (uint32_t)(4 * ihl + 24))
+      st |= kPktBadLen;
+    if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
+    const bool good = (st & kPktFatal) == 0;
+    uint32_t R;
+    if (__all(good && ihl == 5)) {
+      // masks and seed patched in place (every lane reads its dwords before
+      // any writes them: a dead lane's copy of the last frame writes the same
+      // values), then the four chains with the lane's own zero pad in front
+      // (absorbing zeros into a zero register keeps it zero, so shorter
+      // frames just start later)
+      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+      __asm__ __volatile__("" ::: "memory");
+      int nsm = (n + 3) >> 2;
+      const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
+      if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+      }
+      const int ns = __builtin_amdgcn_readfirstlane(nsm);
+      const int pad = 4 * ns - n;
+      const uint32_t pz = pb - 4u * (uint32_t)pad;
+      uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
+        if (j < ns) {  // uniform
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const int kp = 4 * j + cc;
+            const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
+            kk.absorb(P[cc], T[cc], kp >= pad ? w : 0u);
+          }
+        }
+      }
+      R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
+      R = mul_comb(R, kComb) ^ P[1] ^ T[1];
+      R = mul_comb(R, kComb) ^ P[0] ^ T[0];
+    } else {
+      R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
+    }
+    const uint32_t icrc = good ? ~R : 0u;
+    if (live) {
+      if constexpr (VERIFY) {
+        const bool ok = good && trailer == icrc;
+        if (good && !ok) st |= kPktIcrcMismatch;
+        stg8<kCompactStorePol>(a.ok_out + pkt, ok ? 1u : 0u);
+      }
+      if constexpr ((OUTS & 1) != 0) stg32<kCompactStorePol>(a.icrc_out + pkt, icrc);
+      if constexpr ((OUTS & 2) != 0) stg8<kCompactStorePol>(a.status_out + pkt, st);
+    }
+    __asm__ __volatile__("" ::: "memory");
+  };
+  // write a group's span registers into the slot (the slot's previous group
+  // is folded: LDS ops of a wave run in issue order)
+  auto stage = [&](const CGroup& c, const u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
+    const uint32_t last = (c.span + 15u) / 16u - 1u;
+#pragma unroll
+    for (int t = 0; t < kCompactLoads; ++t)
+      *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
+    __asm__ __volatile__("" ::: "memory");
+  };
+
+  // Issue order, so that no wait retires a younger span: step i stages group
+  // i (its span issued two steps before), issues group i + 3's descriptors,
+  // tests group i + 2 (descriptors issued one step before, ahead of group
+  // i + 1's span), issues its span and folds group i.  Descriptors of the
+  // groups two and three ahead ping-pong between (La, oa) and (Lb, ob).
+  uint32_t L0, L1, La, Lb;
+  uint64_t o0, o1, oa, ob;
+  load_desc(0, L0, o0);
+  load_desc(1, L1, o1);
+  load_desc(2, La, oa);
+  u32x4 XA[kCompactLoads], XB[kCompactLoads];
+  CGroup ca = compact_test(a, group(0), L0, o0, lane);
+  issue(ca, XA);
+  CGroup cb = compact_test(a, group(min(1, cnt - 1)), L1, o1, lane);
+  if (cnt < 2) cb.span = 0;
+  issue(cb, XB);
+  // group i in (c, X); the next group's descriptors into (Ln, on); group
+  // i + 2's in (Lt, ot)
+  auto step = [&](int i, CGroup& c, u32x4 (&X)[kCompactLoads], uint32_t& Lt, uint64_t& ot, uint32_t& Ln,
+                  uint64_t& on) __attribute__((always_inline)) {
+    const CGroup cur = c;
+    body_prio_hi();
+    if (cur.span != 0) stage(cur, X);  // (uniform)
+    load_desc(i + 3, Ln, on);
+    c = compact_test(a, group(min(i + 2, cnt - 1)), Lt, ot, lane);
+    if (i + 2 >= cnt) c.span = 0;
+    issue(c, X);
+    body_prio_lo();
+    run(i, cur);
+  };
+  int i = 0;
+  for (; i + 1 < cnt; i += 2) {
+    step(i, ca, XA, La, oa, Lb, ob);
+    step(i + 1, cb, XB, Lb, ob, La, oa);
+  }
+  if (i < cnt) step(i, ca, XA, La, oa, Lb, ob);
+}
+
+// ---------------------------------------------------------------------------
 // Small frames (strided, stride <= kSmallMaxStride): one LANE per packet.
 //
 // With a group of lanes per packet, a 108-byte frame gives each lane a dozen
@@ -2160,6 +2444,20 @@ kernel_fn select_kernel(int log2g, bool ragged, bool verify, bool compact = fals
   }
 }
 
+template <bool V>
+kernel_fn pick_compact(int outs) {
+  switch (outs) {
+    case 0: return icrc_compact_kernel<V, 0>;
+    case 1: return icrc_compact_kernel<V, 1>;
+    case 2: return icrc_compact_kernel<V, 2>;
+    default: return icrc_compact_kernel<V, 3>;
+  }
+}
+kernel_fn select_compact(bool verify, int outs) {
+  return verify ? pick_compact<true>(outs) : pick_compact<false>(outs);
+}
+constexpr size_t kCompactLdsBytes = kCompactSlots + kCompactWaves * kCompactSpan;
+
 size_t lds_bytes(int log2g, bool ragged) {
   if (!ragged) return 163840u;  // tables, fix-up LUT, then the block's ICRC words
   switch (log2g) {
@@ -2257,6 +2555,11 @@ hipError_t prepare_kernels() {
           hipError_t e = set_dynamic_lds((const void*)k, 163840);
           if (e != hipSuccess) return e;
         }
+  for (int v = 0; v < 2; ++v)
+    for (int o = 0; o < 4; ++o) {
+      hipError_t e = set_dynamic_lds((const void*)select_compact(v, o), (int)kCompactLdsBytes);
+      if (e != hipSuccess) return e;
+    }
   hipError_t e = set_dynamic_lds((const void*)icrc_service_kernel, (int)kSvcLds);
   if (e != hipSuccess) return e;
   return prepare_segment_kernels();
@@ -2270,6 +2573,15 @@ hipError_t launch_service(const ServiceArgs& a, hipStream_t stream) {
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
                        hipStream_t stream, bool compact) {
   if (a.n == 0) return hipSuccess;
+  if (ragged && compact && ragged_has_compact(log2g)) {  // the streaming compact kernel
+    const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
+    const uint64_t groups = (a.n + 63) / 64;
+    uint64_t blocks = (groups + kCompactWaves - 1) / kCompactWaves;
+    if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
+    hipLaunchKernelGGL(select_compact(verify, outs), dim3((unsigned)blocks), dim3(kCompactThreads),
+                       kCompactLdsBytes, stream, a);
+    return hipGetLastError();
+  }
   kernel_fn k = select_kernel(log2g, ragged, verify, compact);
   if (!k) return hipErrorInvalidValue;
   const uint32_t ppw = 64u >> log2g;
