@@ -67,7 +67,7 @@ WORKLOADS = {
              "(GPU fault injector hits ~3/1024 frames: ICRC and payload bit flips must fail, "
              "randomised masked fields must pass)"),
     # the responder's dominant frame (src/roce_rq.py:767-776): device-resident
-    # ragged batches of ACKs, the compact tiny-batch phase of the ragged kernel
+    # ragged batches of ACKs, the ragged COMPACT kernel
     "ack": (4, 1 << 24, 0x1C2C0007,
             "ACK frames (IPv4/UDP/BTH/AETH, 48 B) packed back to back, device-resident ragged "
             "ICRC compute (offsets + lengths in HBM)"),
@@ -403,9 +403,9 @@ class RaggedCompute:
         self.d_offs = torch.from_numpy(self.offs.view(np.int64)).to(dev)
         self.d_lens = torch.from_numpy(self.lens.view(np.int32)).to(dev)
         self.out = torch.zeros(n, dtype=torch.int32, device=dev)
-        # the responder knows its stream is ACKs: the ragged kernel with the
-        # compact tiny-batch phase on every launch (not the learned AUTO hint,
-        # which follows the last launch finished before each one)
+        # the responder knows its stream is ACKs: the compact kernel on every
+        # launch (not the learned AUTO hint, which follows the last launch
+        # finished before each one)
         from roce_icrc import engine as E
         eng.set_ragged_variant(E.RAGGED_COMPACT)
 
@@ -814,7 +814,7 @@ def main():
     # variant is fixed per launch on the host, include/roce_icrc.h)
     ragged_kernel = None
     if isinstance(W, (RaggedVerify, RaggedCompute)):
-        ragged_kernel = {1: "compact (tiny-batch phase)", 2: "sorted"}.get(
+        ragged_kernel = {1: "compact", 2: "sorted"}.get(
             eng.last_ragged_variant(), "none")
     ceil_key, ceil_gbps, ceil_ts = ceiling()
     if os.environ.get("ROCE_ICRC_BENCH_TRACE"):  # per-launch times (us) to stderr

@@ -95,25 +95,27 @@ int ricrc_ctx_set_lanes_per_packet(ricrc_ctx* ctx, int lanes);
 /* The hipStream_t the synchronous host-buffer calls run on. */
 void* ricrc_ctx_stream(ricrc_ctx* ctx);
 
-/* Ragged-kernel variant (ABI 5).  The mixed-width ragged kernel (automatic
- * lanes, or 8) comes in two builds: one with the compact tiny-batch phase,
- * which folds packed runs of 64 frames of at most 128 bytes lane-per-packet
- * without the window sort (a responder's ACK / NAK / atomic-ack stream,
- * src/roce_rq.py:767-853), and one without it (every frame through the sort;
- * mixed-MTU data, src/roce_v2.py:327-372).  Both give the same words; each is
- * the faster one for its composition (ACK frames: compact ~1.5x; no tiny
- * frames: sorted 1.5-3.5 %).
+/* Ragged-kernel variant (ABI 5).  Ragged batches (automatic lanes, or 8) run
+ * one of two kernels.  COMPACT streams 64-frame groups: a group whose frames
+ * are 44-128 B, dword-aligned, in order and inside 4 KiB (a responder's ACK /
+ * NAK / atomic-ack stream, src/roce_rq.py:767-853) is folded lane-per-frame
+ * straight from one coalesced span read; any other group is folded by lane
+ * groups, unsorted.  SORTED counting-sorts windows of 8192 frames by length
+ * and folds them in size-homogeneous lane groups (mixed-MTU data,
+ * src/roce_v2.py:327-372).  Both give the same words; each is the faster one
+ * for its composition (2^24 ACK frames: compact 1.25x; mixed MTU: sorted).
  *   RICRC_RAGGED_AUTO     default.  Host-buffer calls decide per call from
- *                         the lengths they hold (compact when at least 1/16
- *                         of the batch's 64-frame groups are all tiny).
- *                         Device-resident calls cannot see the lengths: they
- *                         follow the context's learned hint, which the
- *                         previous ragged launch's first workgroup sets from
- *                         its first 1024 lengths -- so launches enqueued back
- *                         to back follow the last launch FINISHED before them.
- *   RICRC_RAGGED_COMPACT  every ragged launch of the context runs the kernel
- *                         with the compact phase.
- *   RICRC_RAGGED_SORTED   ... the kernel without it.
+ *                         the lengths they hold (compact when at least half
+ *                         of the batch's 64-frame groups hold only frames of
+ *                         at most 128 B).  Device-resident calls cannot see
+ *                         the lengths: they follow the context's learned
+ *                         hint, which the previous ragged launch's first
+ *                         workgroup sets by the same rule from the batch's
+ *                         first groups -- so launches enqueued back to back
+ *                         follow the last launch FINISHED before them.
+ *   RICRC_RAGGED_COMPACT  every ragged launch of the context runs the compact
+ *                         kernel.
+ *   RICRC_RAGGED_SORTED   ... the sorted kernel.
  * A context is single-threaded, so a caller whose device-resident batches
  * alternate composition sets the variant before each call. */
 #define RICRC_RAGGED_AUTO 0
@@ -122,7 +124,8 @@ void* ricrc_ctx_stream(ricrc_ctx* ctx);
 int ricrc_ctx_set_ragged_variant(ricrc_ctx* ctx, int variant);
 /* The variant the context's last ragged launch ran (RICRC_RAGGED_COMPACT or
  * RICRC_RAGGED_SORTED; RICRC_RAGGED_SORTED also for the single-width ragged
- * kernels, which have no compact phase), RICRC_RAGGED_AUTO before any. */
+ * kernels that an explicit lanes setting other than 8 selects),
+ * RICRC_RAGGED_AUTO before any. */
 int ricrc_ctx_last_ragged_variant(ricrc_ctx* ctx, int* variant_out);
 
 /* ---- host buffers, synchronous (H2D + kernel + D2H) --------------------- */

@@ -329,20 +329,21 @@ void service_pause(ricrc_ctx* c) {
   if (c->svc_launched) __atomic_store_n(&c->svc->stop, 1u, __ATOMIC_RELEASE);
 }
 
-// Ragged kernel variant (icrc_ragged_mixed_kernel with or without the compact
-// tiny-batch phase, include/roce_icrc.h RICRC_RAGGED_*).  A variant the caller
-// set wins.  Under AUTO, host-buffer calls decide from the lengths they hold
-// (host_ragged_variant); device-resident calls follow the context's learned
-// hint: each context owns one word of a process-wide host-mapped block, a
-// ragged launch's first workgroup stores into it whether its first 1024
-// packets hold a frame of at most 128 bytes, and the context's later AUTO
+// Ragged kernel variant (include/roce_icrc.h RICRC_RAGGED_*): the compact
+// kernel (icrc_compact_kernel) or the sorted window kernel
+// (icrc_ragged_mixed_kernel).  A variant the caller set wins.  Under AUTO,
+// host-buffer calls decide from the lengths they hold (host_ragged_variant);
+// device-resident calls follow the context's learned hint: each context owns
+// one word of a process-wide host-mapped block, a ragged launch's first
+// workgroup stores into it whether the batch's first 64-packet groups are
+// mostly small frames (store_tiny_hint), and the context's later AUTO
 // launches run the compact kernel while it is 1 (launches enqueued back to
 // back all read what the kernels finished before them wrote; a context's
-// first one runs without the compact phase).  The words are never freed: a
-// kernel launched on a caller's stream may still write one after its context
-// is destroyed (a recycled word then only steers a choice, never a result).
+// first one runs the sorted kernel).  The words are never freed: a kernel
+// launched on a caller's stream may still write one after its context is
+// destroyed (a recycled word then only steers a choice, never a result).
 constexpr uint32_t kHintWords = 4096;
-constexpr uint32_t kTinyFrameLen = 128;  // the compact phase's longest frame
+constexpr uint32_t kTinyFrameLen = 128;  // the compact kernel's longest frame
 std::mutex g_hint_mu;
 uint32_t* g_hints = nullptr;
 uint32_t g_hint_next = 0;
@@ -354,7 +355,7 @@ uint32_t* hint_word() {
   if (!g_hints) {
     void* h = nullptr;
     if (hipHostMalloc(&h, kHintWords * 64u, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-      g_hint_failed = true;  // (no hint: AUTO device launches run without the compact phase, still exact)
+      g_hint_failed = true;  // (no hint: AUTO device launches run the sorted kernel, still exact)
       return nullptr;
     }
     std::memset(h, 0, kHintWords * 64u);
@@ -363,9 +364,11 @@ uint32_t* hint_word() {
   return g_hints + 16u * (g_hint_next++ % kHintWords);  // (one 64-byte line each)
 }
 
-// AUTO for a batch whose lengths are on the host: the compact phase pays for
-// packed runs of tiny frames, so count the 64-frame groups whose frames are
-// all at most 128 bytes; at least 1/16 of the groups selects it.
+// AUTO for a batch whose lengths are on the host: the compact kernel streams
+// 64-frame groups of small frames and folds any other group unsorted, so it
+// is chosen when at least half of the batch's 64-frame groups hold only
+// frames of at most 128 bytes (the kernels' own hint uses the same rule on
+// the batch's first groups, icrc_kernels.hip store_tiny_hint).
 int host_ragged_variant(const uint32_t* lens, uint32_t n) {
   uint32_t groups = 0, tiny = 0;
   for (uint32_t g = 0; g < n; g += 64, ++groups) {
@@ -374,7 +377,7 @@ int host_ragged_variant(const uint32_t* lens, uint32_t n) {
     while (k < e && lens[k] <= kTinyFrameLen) ++k;
     tiny += k == e ? 1u : 0u;
   }
-  return tiny && 16u * tiny >= groups ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
+  return tiny && 2u * tiny >= groups ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
 }
 
 // `host_lens`: the batch's lengths when the caller passed them on the host
@@ -411,8 +414,8 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
         v = host_lens ? host_ragged_variant(host_lens, n)
             : c->tiny_hint && __atomic_load_n(c->tiny_hint, __ATOMIC_ACQUIRE) != 0u ? RICRC_RAGGED_COMPACT
                                                                                     : RICRC_RAGGED_SORTED;
-      // (only the mixed-width kernel has the compact phase)
-      compact = v == RICRC_RAGGED_COMPACT && ricrc::ragged_has_compact(log2g);
+      // (automatic lanes, or 8: an explicit other setting keeps its lane groups)
+      compact = v == RICRC_RAGGED_COMPACT && (c->lanes == 0 || ricrc::ragged_has_compact(log2g));
       c->last_ragged = compact ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
     }
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s, compact));

@@ -38,9 +38,10 @@ struct IcrcArgs {
   // made from the pointer inside the kernel turned every frame load of the
   // kernel into a flat load)
   uint32_t frames_lo4;
-  // ragged mixed kernel: host-mapped word a workgroup sets when its first
-  // packets hold a frame of at most 128 bytes (nullable); the launcher picks
-  // the kernel with phase 0 for the context's next ragged launch from it
+  // ragged kernels: host-mapped word the first workgroup sets when the batch's
+  // first 64-packet groups are mostly frames of at most 128 bytes (nullable);
+  // the launcher picks the compact kernel for the context's next AUTO ragged
+  // launch from it (icrc_kernels.hip store_tiny_hint)
   uint32_t* tiny_hint;
 };
 
@@ -54,8 +55,9 @@ constexpr int kMaxClaimBlocks = 1024;
 // Builds the table image on the host (kTableWords words).
 void build_table_image(uint32_t* out);
 
-// Ragged launches at 8 lanes per packet run the mixed-width kernel, the one
-// built with and without the compact tiny-batch phase (`compact` below).
+// Ragged launches at 8 lanes per packet run the sorted mixed-width kernel;
+// `compact` (below) runs the compact kernel instead, at any lanes choice
+// (include/roce_icrc.h RICRC_RAGGED_*).
 constexpr bool ragged_has_compact(int log2g) { return log2g == 3; }
 
 // Enqueues the ICRC kernel; returns a hipError_t.

@@ -45,8 +45,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <utility>
-
 namespace ricrc {
 
 namespace {
@@ -805,163 +803,18 @@ __device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb
   return fold_masked4<GLOBAL, K, COMB, CH>(f, pb, ihl, n);
 }
 
-// Compact tiny batches ("phase 0", round 4).  The responder's frames (ACK /
-// NAK / atomic ack, 48-56 B, src/roce_rq.py:767-853) come in packed runs: 64
-// consecutive window packets whose frames lie in order, without overlap,
-// inside one 4 KiB span.  Such a batch needs neither the sort nor a lane group:
-// the wave stages the span with 16-byte coalesced loads (4 per lane) into its
-// own LDS slot -- the window's sort arrays, not yet filled -- each lane patches
-// its frame's masked dwords and seed in place and folds the frame from LDS as
-// the small-frame kernel does (four Mul(128) chains, three Mul(-32) Horner
-// steps), and the next batch's span is in flight while this one folds.  The
-// descriptor pass finds the batches (one wave = 64 consecutive packets of one
-// descriptor round) and leaves them out of the sort; each wave folds the
-// compact batches of its OWN descriptor rounds, with the frame lengths and span
-// offsets that test left in its registers (round 4, session t: +6 % on ACK
-// frames against handing the batches round-robin to all waves, which had to
-// read every batch's descriptors a second time; profiles/r04t).
-constexpr uint32_t kCompactSpan = 4096;                        // bytes one wave stages per batch
+// Compact groups (the ragged COMPACT variant, icrc_compact_kernel below): 64
+// consecutive packets whose frames (44-128 B, dword-aligned) lie in order,
+// without overlap, inside one 4 KiB span from the first frame's 16-byte line.
+constexpr uint32_t kCompactSpan = 4096;                        // bytes one wave stages per group
 constexpr int kCompactLoads = (int)(kCompactSpan / 16u / 64u);  // 16-byte loads per lane
-constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a batch may hold
-static_assert(kIcrcWaves * kCompactSpan <= 8u * (uint32_t)MixedLds::kWindow,
-              "every wave's staging slot inside the sort arrays");
-// a batch's words (one coalesced 256-B store per wave) are written
+constexpr uint32_t kCompactMaxLen = 128;                        // longest frame a group may hold
+// a group's words (one coalesced 256-B store per wave) are written
 // non-temporally: ACK bench +1.6-3 % over 3 A/B rounds against the default
 // policy (whole-library nt builds: cfg3 neutral; sc1 -1.5 %; profiles/r04x)
 constexpr int kCompactStorePol = 2;
-// the window's compact batches, entry wave * KR + round: {span start (u64), -, span bytes}
-constexpr uint32_t kCompactList = MixedLds::kBytes;
-constexpr uint32_t kMixedLdsBytes = kCompactList + 16u * (uint32_t)(MixedLds::kWindow / 64);
+constexpr uint32_t kMixedLdsBytes = MixedLds::kBytes;
 static_assert(kMixedLdsBytes <= 163840u, "LDS");
-
-// Phase 0 of one wave: its compact rounds (bit r of cbits: the batch of packets
-// r * threads + wave * 64 + lane), Lr / relr = each lane's frame length and
-// its frame's offset in the round's span, from the descriptor pass.
-template <bool VERIFY, int OUTS, int KR>  // OUTS: 1 = icrc_out, 2 = status_out present
-__device__ __forceinline__ void compact_batches(const IcrcArgs& a, uint32_t w0, int cnt, int wave, int lane,
-                                                uint32_t ok_lds, uint32_t cbits, const uint32_t (&Lr)[KR],
-                                                const uint32_t (&relr)[KR]) {
-  const MixedKeysS kk = MixedKeysS::make(lane);  // Mul(128) is staged in the G = 4 half
-  constexpr uint32_t kComb = MixedKeysS::kComb;   // Mul(-32)
-  // (scalar: a per-lane copy was spilled, and its reload inside the batch
-  // loop waited for the next batch's loads too -- scratch shares vmcnt)
-  const uint32_t slot =
-      MixedLds::kPerm + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * kCompactSpan;
-  struct Ent {
-    uint64_t b16;
-    uint32_t span;
-  };
-  auto entry = [&](uint32_t r) {
-    const u32x4 v = *(const lds_u32x4*)(uintptr_t)(kCompactList + 16u * ((uint32_t)wave * KR + r));
-    Ent e;
-    e.b16 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.x) |
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.y) << 32);
-    e.span = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
-    return e;
-  };
-  // a batch's span chunks (unconditional, clamped)
-  auto issue = [&](const Ent& e, u32x4* X) __attribute__((always_inline)) {
-    const uint32_t last = (e.span + 15u) / 16u - 1u;
-    const uint8_t* base = a.frames + (e.b16 - a.frames_lo4);  // (b16: from the line below frames)
-#pragma unroll
-    for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
-  };
-  uint32_t todo = cbits;
-  if (todo == 0u) return;
-  u32x4 X[kCompactLoads];
-  Ent cur = entry((uint32_t)__builtin_ctz(todo));
-  issue(cur, X);
-#pragma unroll
-  for (int r = 0; r < KR; ++r) {
-    if ((cbits >> r) & 1u) {  // (uniform)
-      const Ent e = cur;
-      const uint32_t last = (e.span + 15u) / 16u - 1u;
-      body_prio_hi();
-#pragma unroll
-      for (int t = 0; t < kCompactLoads; ++t)
-        *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
-      __asm__ __volatile__("" ::: "memory");  // LDS ops of a wave run in issue order
-      todo &= ~(1u << r);
-      if (todo) {  // (uniform) the next compact round's span, in flight during this fold
-        cur = entry((uint32_t)__builtin_ctz(todo));
-        issue(cur, X);
-      }
-      body_prio_lo();
-      const uint32_t L = Lr[r];
-      // (an opaque lane id per round: the compiler otherwise hoisted the
-      // output addresses of all rounds and spilled them)
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      const uint32_t i = (uint32_t)(r * kIcrcThreads + wave * 64 + ln);
-      const bool live = i < (uint32_t)cnt;
-      const uint32_t pb = slot + relr[r];
-      const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the descriptor pass checked every lane)
-      const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
-      const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
-      uint32_t st = 0;
-      const int ihl = (int)(d0 & 0xFu);
-      if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
-        st |= kPktNotIpv4;
-      else if (((d2 >> 8) & 0xFFu) != 17u)
-        st |= kPktNotUdp;
-      else if (L < (uint32_t)(4 * ihl + 24))
-        st |= kPktBadLen;
-      if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
-      const bool good = (st & kPktFatal) == 0;
-      uint32_t R;
-      if (__all(good && ihl == 5)) {
-        // every frame IHL 5: masks and seed patched in place, then the four
-        // chains with the lane's own zero pad in front (absorbing zeros into a
-        // zero register keeps it zero, so shorter frames just start later)
-        lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
-        lds_wr(pb + 8, d2 | 0xFFFF00FFu);
-        lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
-        lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
-        __asm__ __volatile__("" ::: "memory");
-        int nsm = (n + 3) >> 2;
-        const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
-        if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
-#pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
-        }
-        const int ns = __builtin_amdgcn_readfirstlane(nsm);
-        const int pad = 4 * ns - n;
-        const uint32_t pz = pb - 4u * (uint32_t)pad;
-        uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
-          if (j < ns) {  // uniform
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              const int kp = 4 * j + c;
-              const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
-              kk.absorb(P[c], T[c], kp >= pad ? w : 0u);
-            }
-          }
-        }
-        R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
-        R = mul_comb(R, kComb) ^ P[1] ^ T[1];
-        R = mul_comb(R, kComb) ^ P[0] ^ T[0];
-      } else {
-        R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
-      }
-      const uint32_t icrc = good ? ~R : 0u;
-      if (live) {
-        if constexpr (VERIFY) {
-          const bool ok = good && trailer == icrc;
-          if (good && !ok) st |= kPktIcrcMismatch;
-          lds_wr8(ok_lds + i, ok ? 1u : 0u);
-        }
-        // (OUTS is a template parameter: a store under a run-time test leaves
-        // the compiler a variable count of stores after the next batch's loads,
-        // and its wait for them then waits for the stores as well)
-        if constexpr ((OUTS & 1) != 0) stg32<kCompactStorePol>(a.icrc_out + w0 + i, icrc);
-        if constexpr ((OUTS & 2) != 0) stg8<kCompactStorePol>(a.status_out + w0 + i, st);
-      }
-      __asm__ __volatile__("" ::: "memory");
-    }
-  }
-}
 
 template <int LOG2G, bool VERIFY, class K>
 __device__ __forceinline__ void mixed_set(const IcrcArgs& a, int s, int e, uint32_t w0, int lane,
@@ -990,9 +843,10 @@ __device__ __forceinline__ void mixed_set(const IcrcArgs& a, int s, int e, uint3
   finish_packet<LOG2G, VERIFY, K, kMixedLut>(a, p, b, gl, grp * G, kk, ob);
 }
 
-// The workgroup's windows.  COMPACT: with the compact tiny batches (phase 0)
-// and their per-round test; without, the round-3 window loop.
-template <bool VERIFY, bool COMPACT>
+// The workgroup's windows.  (Round 4's compact tiny batches inside the
+// windows -- "phase 0" -- became a kernel of their own in round 5,
+// icrc_compact_kernel below.)
+template <bool VERIFY>
 __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
   constexpr int DPI = 32;  // sort key: G = 8 iterations
   using LD = MixedLds;
@@ -1011,10 +865,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
   constexpr uint32_t kNoOff = 0xFFFFFFFFu;
   lds_u32* claim = (lds_u32*)(uintptr_t)(LD::kBase - 4u);  // (free words at the end of the LUT)
   lds_u32* tclaim = (lds_u32*)(uintptr_t)(LD::kBase - 8u);  // phase A's claim counter
-  lds_u32* ncompact = (lds_u32*)(uintptr_t)(LD::kBase - 12u);  // phase 0: batches listed
-  lds_u32* ncompact_pkts = (lds_u32*)(uintptr_t)(LD::kBase - 16u);  // ... and their packets
   const bool from_back = ((tid >> 6) & 1) != 0;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (scalar: its per-lane copies were spilled)
   bool s_tiny = false;  // (uniform) the G = 4 half holds Mul(128) instead of Mul(512)
 
   const uint32_t nwin = p1 > p0 ? (p1 - p0 + W - 1) / W : 1;
@@ -1025,9 +876,8 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
   // every descriptor load of the thread first (clamped, unconditional: a
   // guarded load makes the compiler wait for each in turn)
   auto load_descriptors = [&](uint32_t w, int n) __attribute__((always_inline)) {
-    // (an opaque window start: the compiler otherwise kept the addresses of
-    // the window's first loads for the reload after phase 0, 16 VGPR pairs
-    // live across it, and spilled them)
+    // (an opaque window start, which the round-4 phase 0 needed against
+    // spills; kept: the sorted kernel's code is unchanged by it)
     asm volatile("" : "+s"(w));
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
@@ -1051,62 +901,14 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
     if (tid < NB) hist[tid] = 0;
     if (tid == NB) *claim = 0;
     if (tid == NB + 1) *tclaim = 0;
-    if constexpr (COMPACT) {
-      if (tid == NB + 2) *ncompact = 0;
-      if (tid == NB + 3) *ncompact_pkts = 0;
-    }
     __syncthreads();
     int keys[KR];
     uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
     load_descriptors(w0, cnt);
-    uint32_t cbits = 0;  // (uniform) bit r: round r's batch is compact
-    uint32_t relr[KR];   // a compact round's frame offset in its span (phase 0)
-    // Phase 0's test, per descriptor round (wave-uniform: the wave's 64
-    // packets of the round): every live frame tiny, dword-aligned, after its
-    // left neighbour's end, and inside the 4 KiB from the first frame's
-    // 16-byte line.
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
-      bool compact = false;
-      // (uniform) lane 0 is live, and some frame of the round is tiny (a
-      // window without tiny frames pays one compare and one ballot per round)
-      if (COMPACT && r * kIcrcThreads + wave * 64 < cnt && __any(Lr[r] <= kCompactMaxLen)) {
-        const int nlive = min(64, cnt - (r * kIcrcThreads + wave * 64));  // (uniform)
-        const bool live = lane < nlive;
-        const uint32_t L = Lr[r];
-        const uint64_t addr = a.frames_lo4 + Or[r];  // (from the line below frames)
-        const uint64_t b16 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr) |
-                              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr >> 32))
-                               << 32)) & ~15ull;
-        // offsets inside the 4 KiB from b16 (a frame outside fails the test)
-        const uint64_t rel64 = addr - b16;
-        const uint32_t rel = rel64 < kCompactSpan ? (uint32_t)rel64 : 0xFFFF0000u;
-        const uint32_t end = rel + L;
-        // the left neighbour's end: one DPP wave shift (lane 0 gets 0)
-        const uint32_t prev_end =
-            (uint32_t)__builtin_amdgcn_update_dpp(0, (int)end, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
-        const bool ok = !live || (L >= 44 && L <= kCompactMaxLen && (L & 3u) == 0 && (rel & 3u) == 0 &&
-                                  end <= kCompactSpan && rel >= prev_end);
-        compact = __all(ok);
-        relr[r] = rel;
-        if (compact) {
-          cbits |= 1u << r;
-          // in order without overlap: the last live frame ends the span
-          const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)end, nlive - 1);
-          if (lane == 0) {
-            atomicAdd((uint32_t*)ncompact, 1u);
-            // (an opaque third word: as a constant the compiler kept one
-            // 16-byte entry template per round live across the window loop)
-            uint32_t z = 0;
-            asm volatile("" : "+v"(z));
-            *(lds_u32x4*)(uintptr_t)(kCompactList + 16u * (uint32_t)(wave * KR + r)) =
-                u32x4{(uint32_t)b16, (uint32_t)(b16 >> 32), z, span};
-            atomicAdd((uint32_t*)ncompact_pkts, (uint32_t)nlive);
-          }
-        }
-      }
-      // sort key, offset / 4 and length of window packet i (key -1: a
-      // compact batch's packet, left out of the sort)
+      const bool compact = false;  // (round 4: the packet of a compact batch)
+      // sort key, offset / 4 and length of window packet i
       const int i = tid + r * kIcrcThreads;
       int key = 0;
       offw[r] = kNoOff;
@@ -1128,12 +930,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
       const bool counted = i < cnt && !compact;
       if (counted) atomicAdd((uint32_t*)&hist[keys[r]], 1u);
     }
-    if constexpr (!COMPACT) {
-      kill_descriptors();
-    } else {
-#pragma unroll
-      for (int r = 0; r < KR; ++r) Or[r] = __builtin_nondeterministic_value(Or[r]);
-    }
+    kill_descriptors();
     __syncthreads();
     OutBuf ob = {0, 0};
     if constexpr (VERIFY) {
@@ -1141,69 +938,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
       ob.ok_cap = (uint32_t)cnt;
       ob.ok_lds = LD::kOk;
     }
-    // ---- phase 0: the compact tiny batches, before the sort fills the arrays
-    // their waves stage through; the rest of the window (cs packets) is sorted
-    int cs = cnt;  // (uniform) the packets the sort phases take
-    if constexpr (COMPACT) {
-    const int ncb = (int)__builtin_amdgcn_readfirstlane((int)*ncompact);
-    cs = cnt - (int)__builtin_amdgcn_readfirstlane((int)*ncompact_pkts);
-    if (ncb > 0) {
-      // keys / offw / lw hold no value across phase 0 (recomputed after it)
-#pragma unroll
-      for (int r = 0; r < KR; ++r) {
-        keys[r] = __builtin_nondeterministic_value(keys[r]);
-        offw[r] = __builtin_nondeterministic_value(offw[r]);
-        lw[r] = __builtin_nondeterministic_value(lw[r]);
-      }
-      if (!s_tiny) {
-        MixedKeysS::template stage<kIcrcThreads>(a.tables + 0 * 1024, tid);  // main set 0: Mul(128)
-        s_tiny = true;
-        __syncthreads();
-      }
-      // (Lr and relr are phase 0's lengths and span offsets; Or is dead)
-      if (a.icrc_out && a.status_out)
-        compact_batches<VERIFY, 3, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
-      else if (a.icrc_out)
-        compact_batches<VERIFY, 1, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
-      else if (a.status_out)
-        compact_batches<VERIFY, 2, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
-      else
-        compact_batches<VERIFY, 0, KR>(a, w0, cnt, wave, lane, LD::kOk, cbits, Lr, relr);
-      __syncthreads();  // the staging slots are the sort arrays again
-      if (cs == 0) {  // (uniform) a window of compact batches only: nothing to sort
-        if constexpr (VERIFY) {
-          // (the next window's barrier precedes its first verdict write)
-          for (int i = tid; i < cnt; i += kIcrcThreads) a.ok_out[w0 + i] = (uint8_t)lds_rd8(LD::kOk + i);
-        }
-        continue;
-      }
-      // the sort's descriptors again (L2 hits) and its keys
-      load_descriptors(w0, cnt);
-#pragma unroll
-      for (int r = 0; r < KR; ++r) {
-        const bool compact = (cbits >> r) & 1u;
-        const int i = tid + r * kIcrcThreads;
-        int key = 0;
-        offw[r] = kNoOff;
-        lw[r] = 0;
-        if (i < cnt && !compact) {
-          const uint32_t L = Lr[r];
-          const uint64_t off = Or[r];
-          if (off < (1ull << 34) && (off & 3u) == 0) offw[r] = (uint32_t)(off >> 2);
-          lw[r] = L > 65535u ? 0u : L;  // (0: unusable, as L > 65535 is)
-          if (!(L < 44 || (L & 3u) || L > 65535u || ((uintptr_t)(a.frames + off) & 3u))) {
-            const int S = (int)(((uintptr_t)(a.frames + off) >> 2) & (DPI - 1));
-            // bucket 0: tiny frames (and unusable ones, which cost nothing)
-            key = L <= kTinyLen ? 0 : min(NB - 1, 1 + (S + (int)((L - 4) >> 2) + DPI - 1) / DPI);
-          }
-        }
-        keys[r] = compact ? -1 : key;
-      }
-    }
-    kill_descriptors();  // (dead on every path from here to the next window's load)
-#pragma unroll
-    for (int r = 0; r < KR; ++r) relr[r] = __builtin_nondeterministic_value(relr[r]);
-    }  // COMPACT
+    const int cs = cnt;  // (uniform) the packets the sort phases take
     // (uniform) the window's tiny frames, sorted to its front
     const int ntiny_all = (int)__builtin_amdgcn_readfirstlane((int)hist[0]);
     const int ntiny = ntiny_all >= kTinyMin ? ntiny_all : 0;
@@ -1311,17 +1046,29 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
   }
 }
 
-// Two kernels: with phase 0 (COMPACT) and without -- the round-3 window loop.
-// In one kernel, the phase-0 code cost cfg3 (no tiny frame) 1.5-3.5 %
-// (register allocation and layout, not work: profiles/r04i, r04j), and one
-// kernel holding both loops spilled the compact loop's descriptors (ACK
-// frames -7 %).  The launch's first workgroup probes its first kIcrcThreads
-// lengths while the tables are staged and stores into the context's hint word
-// whether one of them is at most kCompactMaxLen bytes (one store over PCIe per
-// launch: a store per wave made the ACK kernel 2.9x slower); the launcher
-// picks the kernel of the context's later ragged launches from it
-// (icrc_capi.cpp hint_word; both give the same words).
-template <bool VERIFY, bool COMPACT>
+// The AUTO hint of the ragged launches (icrc_capi.cpp hint_word): the
+// launch's first workgroup looks at the batch's first 64-packet groups, one
+// per wave (`probe`: the thread's packet length), and stores into the
+// context's host-mapped word whether at least half of them hold only frames
+// of at most kCompactMaxLen bytes -- the compact kernel's candidates.  One
+// store over PCIe per launch (a store per wave made the kernel 2.9x slower,
+// round 4); `scratch`: one LDS word per wave, free at this point.
+template <int WAVES>
+__device__ __forceinline__ void store_tiny_hint(uint32_t* hint, uint32_t scratch, int tid, uint32_t probe) {
+  if ((tid & 63) == 0) lds_wr(scratch + 4u * (uint32_t)(tid >> 6), __all(probe <= kCompactMaxLen) ? 1u : 0u);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t tiny = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) tiny += lds_rd(scratch + 4u * (uint32_t)w);
+    __hip_atomic_store(hint, 2u * tiny >= (uint32_t)WAVES ? 1u : 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The SORTED variant: the window loop above (the compact variant is
+// icrc_compact_kernel below).
+template <bool VERIFY>
 __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
   const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
@@ -1331,20 +1078,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   announce_batch(a.busy);
   stage_tables<3, kIcrcThreads, MixedKeysL>(a.tables, tid);
   MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
-  if (a.tiny_hint && blockIdx.x == 0) {  // (uniform) one store over PCIe per launch
-    // the workgroup's OR through one word per wave in the compact list (free
-    // until the first window's test; __syncthreads_or would bring a static
-    // LDS variable, which would sit under the tables)
-    if ((tid & 63) == 0) lds_wr(kCompactList + 4u * (uint32_t)(tid >> 6), __any(probe <= kCompactMaxLen) ? 1u : 0u);
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t any = 0;
-#pragma unroll
-      for (int w = 0; w < kIcrcWaves; ++w) any |= lds_rd(kCompactList + 4u * (uint32_t)w);
-      __hip_atomic_store(a.tiny_hint, any ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  mixed_windows<VERIFY, COMPACT>(a, tid);
+  // (uniform) the hint; scratch: the window's sort arrays, not yet in use
+  if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kIcrcWaves>(a.tiny_hint, MixedLds::kPerm, tid, probe);
+  mixed_windows<VERIFY>(a, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -1461,17 +1197,8 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
   const uint32_t probe = blockIdx.x == 0 ? a.lens[min((uint32_t)tid, a.n - 1u)] : 0xFFFFFFFFu;
   stage_tables<3, kCompactThreads, MixedKeysL>(a.tables, tid);
   MixedKeysS::template stage<kCompactThreads>(a.tables + 0 * 1024, tid);
-  if (a.tiny_hint && blockIdx.x == 0) {  // (uniform) the AUTO hint, as the window kernel stores it
-    if ((tid & 63) == 0)
-      lds_wr(kCompactSlots + 4u * (uint32_t)(tid >> 6), __any(probe <= kCompactMaxLen) ? 1u : 0u);
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t any = 0;
-#pragma unroll
-      for (int w = 0; w < kCompactWaves; ++w) any |= lds_rd(kCompactSlots + 4u * (uint32_t)w);
-      __hip_atomic_store(a.tiny_hint, any ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  // (uniform) the AUTO hint; scratch: the staging slots, not yet in use
+  if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kCompactWaves>(a.tiny_hint, kCompactSlots, tid, probe);
   __syncthreads();
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1712,13 +1439,7 @@ constexpr int kSmallOutRounds = 64;  // output ring depth in rounds (0 = off)
 // 0.320-0.344.
 constexpr int kSmallOutPol = 16;
 
-// NS > 0: the fold's step count ceil(n / 2) fixed at compile time (packed
-// batches, stride == frame length, launch_icrc_small): every per-dword read
-// and step of the unrolled fold is unconditional.  NS = 0 takes it from the
-// frame length at run time, one uniform branch per dword -- with 92 SGPRs
-// spilled into VGPR lanes on top (cfg5 kernel: 6570 instructions, 4308 with
-// NS = 13).
-template <int C, int NS, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
+template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
   const uint32_t S = (uint32_t)a.stride, L = a.len;
@@ -1726,9 +1447,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   const bool dead = L < 44 || (L & 3u) || L > 65535u || L > S;
   constexpr int CH = kSmallChains;
   const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
-  // steps, zero dwords in front (0 or 1); with NS the launcher checked that
-  // the frames are not `dead` and that ceil(n / CH) == NS
-  const int ns = NS > 0 ? NS : (n + CH - 1) / CH, pad = CH * ns - n;
+  const int ns = (n + CH - 1) / CH, pad = CH * ns - n;  // steps, zero dwords in front (0 or 1)
   {
     const uint32_t* m64 = a.tables + kMul64Set * 1024;  // Mul(32 CH)
     for (int i = tid; i < 2048; i += (int)blockDim.x) {  // 8 copies of 1024 words, 2 quads
@@ -1844,11 +1563,10 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* base = a.frames + (uint64_t)min(b, lim) * 64u * S;
     // LDS-DMA straight into the wave's slot: chunk lane + 64 t of the batch
     // lands at stage + 1024 t + 16 lane; lanes past the batch's last chunk
-    // stay idle (the slot holds exactly the batch; with NS, frames of at
-    // least 8 NS bytes, the first 32 NS / 64 loads are whole without a test)
+    // stay idle (the slot holds exactly the batch)
 #pragma unroll
     for (int t = 0; t < C; ++t)
-      if ((NS > 0 && 64 * t + 64 <= 32 * NS) || (uint32_t)(lane + 64 * t) < nchunk)
+      if ((uint32_t)(lane + 64 * t) < nchunk)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(base + 16u * (uint32_t)(lane + 64 * t)),
             (__attribute__((address_space(3))) void*)(uintptr_t)(stage + 1024u * (uint32_t)t), 16, 0, 2);
@@ -2422,24 +2140,22 @@ __global__ void __launch_bounds__(kSvcThreads, 1) icrc_service_kernel(ServiceArg
 typedef void (*kernel_fn)(IcrcArgs);
 
 template <int LOG2G>
-kernel_fn pick(bool ragged, bool verify, bool compact) {
-  if (ragged && ragged_has_compact(LOG2G)) {  // the mixed-width kernel
-    if (compact) return verify ? icrc_ragged_mixed_kernel<true, true> : icrc_ragged_mixed_kernel<false, true>;
-    return verify ? icrc_ragged_mixed_kernel<true, false> : icrc_ragged_mixed_kernel<false, false>;
-  }
+kernel_fn pick(bool ragged, bool verify) {
+  if (ragged && ragged_has_compact(LOG2G))  // the mixed-width kernel (SORTED)
+    return verify ? icrc_ragged_mixed_kernel<true> : icrc_ragged_mixed_kernel<false>;
   if (ragged) return verify ? icrc_ragged_kernel<LOG2G, true> : icrc_ragged_kernel<LOG2G, false>;
   return verify ? icrc_strided_kernel<LOG2G, true> : icrc_strided_kernel<LOG2G, false>;
 }
 
-kernel_fn select_kernel(int log2g, bool ragged, bool verify, bool compact = false) {
+kernel_fn select_kernel(int log2g, bool ragged, bool verify) {
   switch (log2g) {
-    case 0: return pick<0>(ragged, verify, compact);
-    case 1: return pick<1>(ragged, verify, compact);
-    case 2: return pick<2>(ragged, verify, compact);
-    case 3: return pick<3>(ragged, verify, compact);
-    case 4: return pick<4>(ragged, verify, compact);
-    case 5: return pick<5>(ragged, verify, compact);
-    case 6: return pick<6>(ragged, verify, compact);
+    case 0: return pick<0>(ragged, verify);
+    case 1: return pick<1>(ragged, verify);
+    case 2: return pick<2>(ragged, verify);
+    case 3: return pick<3>(ragged, verify);
+    case 4: return pick<4>(ragged, verify);
+    case 5: return pick<5>(ragged, verify);
+    case 6: return pick<6>(ragged, verify);
     default: return nullptr;
   }
 }
@@ -2474,10 +2190,10 @@ size_t lds_bytes(int log2g, bool ragged) {
 template <int C, bool V>
 kernel_fn pick_small(int outs) {
   switch (outs) {
-    case 0: return icrc_small_kernel<C, 0, V, 0>;
-    case 1: return icrc_small_kernel<C, 0, V, 1>;
-    case 2: return icrc_small_kernel<C, 0, V, 2>;
-    default: return icrc_small_kernel<C, 0, V, 3>;
+    case 0: return icrc_small_kernel<C, V, 0>;
+    case 1: return icrc_small_kernel<C, V, 1>;
+    case 2: return icrc_small_kernel<C, V, 2>;
+    default: return icrc_small_kernel<C, V, 3>;
   }
 }
 
@@ -2487,33 +2203,6 @@ kernel_fn select_small(int C, bool verify, int outs) {
   return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
 }
 
-// Exact-step instantiations of packed batches (stride == frame length L):
-// C = 4 for 44-64-B frames (NS 5-8), 7 for 68-112 B (NS 8-14), 8 for
-// 116-128 B (NS 14-16), for the device-resident forms -- compute with ICRC
-// words only, verify with verdicts (with or without the words).  Other output
-// sets, and strides wider than the frames, take NS = 0.
-template <int C, int NS>
-kernel_fn pick_small_exact(bool verify, int outs) {
-  if (!verify && outs == 1) return icrc_small_kernel<C, NS, false, 1>;
-  if (verify && outs == 0) return icrc_small_kernel<C, NS, true, 0>;
-  if (verify && outs == 1) return icrc_small_kernel<C, NS, true, 1>;
-  return nullptr;
-}
-
-template <int C, int NS0, int... K>
-kernel_fn select_small_exact_in(int ns, bool verify, int outs, std::integer_sequence<int, K...>) {
-  kernel_fn k = nullptr;
-  ((ns == NS0 + K ? (k = pick_small_exact<C, NS0 + K>(verify, outs)) : k), ...);
-  return k;
-}
-
-// nullptr: no exact instantiation for this (C, step count, output set)
-kernel_fn select_small_exact(int C, int ns, bool verify, int outs) {
-  if (C == 4) return select_small_exact_in<4, 5>(ns, verify, outs, std::make_integer_sequence<int, 4>{});
-  if (C == 7) return select_small_exact_in<7, 8>(ns, verify, outs, std::make_integer_sequence<int, 7>{});
-  if (C == 8) return select_small_exact_in<8, 14>(ns, verify, outs, std::make_integer_sequence<int, 3>{});
-  return nullptr;
-}
 
 }  // namespace
 
@@ -2536,25 +2225,16 @@ hipError_t set_dynamic_lds(const void* fn, int bytes) {
 hipError_t prepare_kernels() {
   for (int l = 0; l <= kMaxLog2G; ++l)
     for (int r = 0; r < 2; ++r)
-      for (int v = 0; v < 2; ++v)
-        for (int c = 0; c < 2; ++c) {
-          hipError_t e = set_dynamic_lds((const void*)select_kernel(l, r, v, c), (int)lds_bytes(l, r));
-          if (e != hipSuccess) return e;
-        }
+      for (int v = 0; v < 2; ++v) {
+        hipError_t e = set_dynamic_lds((const void*)select_kernel(l, r, v), (int)lds_bytes(l, r));
+        if (e != hipSuccess) return e;
+      }
   for (int c : {4, 7, 8})
     for (int v = 0; v < 2; ++v)
       for (int o = 0; o < 4; ++o) {
         hipError_t e = set_dynamic_lds((const void*)select_small(c, v, o), 163840);
         if (e != hipSuccess) return e;
       }
-  for (int c : {4, 7, 8})
-    for (int ns = 1; ns <= kSmallMaxSteps; ++ns)
-      for (int v = 0; v < 2; ++v)
-        for (int o = 0; o < 2; ++o)
-          if (kernel_fn k = select_small_exact(c, ns, v, o)) {
-          hipError_t e = set_dynamic_lds((const void*)k, 163840);
-          if (e != hipSuccess) return e;
-        }
   for (int v = 0; v < 2; ++v)
     for (int o = 0; o < 4; ++o) {
       hipError_t e = set_dynamic_lds((const void*)select_compact(v, o), (int)kCompactLdsBytes);
@@ -2573,7 +2253,7 @@ hipError_t launch_service(const ServiceArgs& a, hipStream_t stream) {
 hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, int num_cus,
                        hipStream_t stream, bool compact) {
   if (a.n == 0) return hipSuccess;
-  if (ragged && compact && ragged_has_compact(log2g)) {  // the streaming compact kernel
+  if (ragged && compact) {  // the streaming compact kernel (any lanes setting: its own)
     const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
     const uint64_t groups = (a.n + 63) / 64;
     uint64_t blocks = (groups + kCompactWaves - 1) / kCompactWaves;
@@ -2582,7 +2262,7 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
                        kCompactLdsBytes, stream, a);
     return hipGetLastError();
   }
-  kernel_fn k = select_kernel(log2g, ragged, verify, compact);
+  kernel_fn k = select_kernel(log2g, ragged, verify);
   if (!k) return hipErrorInvalidValue;
   const uint32_t ppw = 64u >> log2g;
   const uint64_t nsets = (a.n + ppw - 1) / ppw;
@@ -2604,11 +2284,7 @@ hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStr
   // 16-byte LDS address)
   const int C = a.stride <= 64 ? 4 : a.stride <= 112 ? 7 : 8;
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
-  kernel_fn k = nullptr;
-  const uint32_t L = a.len;
-  if (L == a.stride && L >= 44 && (L & 3u) == 0)  // packed, and not `dead` (L <= stride <= 128)
-    k = select_small_exact(C, (int)(((L - 4) / 4 + kSmallChains - 1) / kSmallChains), verify, outs);
-  if (!k) k = select_small(C, verify, outs);
+  kernel_fn k = select_small(C, verify, outs);
   const uint32_t slot = 64u * (uint32_t)a.stride;
   uint32_t nw = min((uint32_t)kSmallMaxWaves, (kSmallEnd - kSmallStage) / slot);
   if (nw > 2 && (nw & 1u)) --nw;  // even: every SIMD the same number of waves

@@ -338,9 +338,10 @@ class IcrcEngine:
         return float(int(t[1]) - int(t[0])) * 0.01, int(t[2])
 
     def set_ragged_variant(self, variant: int) -> None:
-        """RAGGED_AUTO (default), RAGGED_COMPACT (the ragged kernel with the
-        compact tiny-batch phase: packed ACK / NAK runs) or RAGGED_SORTED
-        (without it) for this engine's ragged launches (include/roce_icrc.h)."""
+        """RAGGED_AUTO (default), RAGGED_COMPACT (the compact kernel: packed
+        ACK / NAK runs streamed in 64-frame groups) or RAGGED_SORTED (the
+        sorted window kernel: mixed-MTU data) for this engine's ragged
+        launches (include/roce_icrc.h)."""
         self._check("ricrc_ctx_set_ragged_variant",
                     self.lib.ricrc_ctx_set_ragged_variant(self.ctx, variant))
 

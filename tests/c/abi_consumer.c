@@ -65,8 +65,7 @@ static int gpu_leg(ricrc_ctx* ctx, int ndev) {
     uint32_t vc[3] = {0, 0, 0};
     if (ricrc_compute_batch(ctx, buf, sizeof buf, offs, lens, 3, vc, NULL) != RICRC_OK) return 37;
     if (vc[0] != out[0] || vc[1] != out[1] || vc[2] != out[2]) return 38;
-    /* (48-B frames on the host run the one-lane ragged kernel: no compact phase) */
-    if (ricrc_ctx_last_ragged_variant(ctx, &v) != RICRC_OK || v != RICRC_RAGGED_SORTED) return 41;
+    if (ricrc_ctx_last_ragged_variant(ctx, &v) != RICRC_OK || v != RICRC_RAGGED_COMPACT) return 41;
     if (ricrc_ctx_set_ragged_variant(ctx, RICRC_RAGGED_AUTO) != RICRC_OK) return 39;
     if (ricrc_ctx_set_service(ctx, 1000) != RICRC_OK) return 40;
   }

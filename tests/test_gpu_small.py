@@ -102,8 +102,7 @@ def test_small_kernel_verify(engine, n):
 
 def _dev_strided(engine, buf, L, n, verify):
     """Device-resident packed batch (stride == L): compute with ICRC words only
-    (the exact-step kernel of the compute form), or verify with verdicts only
-    and with verdicts + words (its two verify forms)."""
+    (bench.py's form), or verify with verdicts only and with verdicts + words."""
     import torch
     dev = torch.device("cuda", 0)
     d = torch.from_numpy(buf).to(dev)
@@ -123,12 +122,12 @@ def _dev_strided(engine, buf, L, n, verify):
 
 
 @pytest.mark.parametrize("L", list(range(44, 129, 4)))
-def test_exact_step_kernels_every_packed_length(engine, L):
-    """Packed batches (stride == frame length) run kernels whose fold step
-    count is a compile-time constant (icrc_small_kernel<C, NS>, NS =
-    ceil((L - 4) / 8)): every length 44..128 B, batch counts across the
-    64-packet batch, ring and last-batch boundaries, compute and both verify
-    forms, against the oracle."""
+def test_device_resident_every_packed_length(engine, L):
+    """Packed batches (stride == frame length) through the device-resident
+    forms: every length 44..128 B (every chunk count and front pad of the
+    two-chain fold), batch counts across the 64-packet batch, output-ring and
+    last-batch boundaries, compute and both verify forms, against the
+    oracle."""
     rng = np.random.default_rng(L)
     for n in (1, 63, 64, 65, 4099, 70001):
         buf = _strided(n, L, L, rng) if n <= 4099 else np.tile(_strided(4099, L, L, rng),
@@ -151,10 +150,10 @@ def test_exact_step_kernels_every_packed_length(engine, L):
 
 
 @pytest.mark.parametrize("L", [48, 68, 108, 128])
-def test_exact_step_kernels_options_and_malformed(engine, L):
-    """The exact-step kernels' batches holding IPv4-option or malformed frames
-    fold from HBM through the per-dword masks (the slot already holds the next
-    batch): ICRC words against the oracle, malformed frames 0."""
+def test_device_resident_options_and_malformed(engine, L):
+    """Batches holding IPv4-option or malformed frames fold from HBM through
+    the per-dword masks (the slot already holds the next batch): ICRC words
+    against the oracle, malformed frames 0."""
     n = 64 * 50 + 9
     rng = np.random.default_rng(L + 1)
     buf = _strided(n, L, L, rng, ihl6_every=29, bad_every=31)

@@ -137,7 +137,7 @@ def test_window_sequences_switch_the_table_half(engine):
 
 def _dev_compute(engine, buf, offs, lens, variant=E.RAGGED_COMPACT):
     """compute_batch_dev with status: (icrc, status) as numpy, on the ragged
-    kernel variant asked for (default: the one with the compact phase, whose
+    kernel variant asked for (default: the compact kernel, whose
     tests these are -- independent of what the engine ran before)."""
     torch = pytest.importorskip("torch")
     n = lens.size
@@ -157,11 +157,12 @@ def _dev_compute(engine, buf, offs, lens, variant=E.RAGGED_COMPACT):
 
 
 def test_compact_ack_batches(engine):
-    """Phase 0 (round 4): packed runs of ACK-sized frames (64 consecutive
-    packets in order inside 4 KiB) are staged and folded lane-per-packet
-    without the sort.  All-ACK batches with a partial last batch and several
-    windows per workgroup, plus 44-64 B mixes; compute and verify (corrupted
-    trailers and payloads flagged) against the oracle."""
+    """The compact kernel's groups: packed runs of ACK-sized frames (64
+    consecutive packets in order inside 4 KiB) are staged and folded
+    lane-per-packet without a sort.  All-ACK batches with a partial last
+    group and many groups per wave, plus 44-64 B mixes; compute and verify
+    (corrupted trailers and payloads flagged) against the oracle, on both
+    variants."""
     rng = np.random.default_rng(21)
     for n, choices in ((100003, [48]), (1 << 22, [48]), (300001, [44, 48, 52, 56, 60, 64])):
         lens = rng.choice(choices, n).astype(np.uint32)
@@ -175,10 +176,10 @@ def test_compact_ack_batches(engine):
 
 
 def test_compact_batches_malformed_and_options(engine):
-    """Frames inside compact batches that leave the IHL-5 fast path: IPv4
+    """Frames inside compact groups that leave the IHL-5 fast path: IPv4
     options (IHL 6), not IPv4, not UDP, a wrong IP total length.  ICRC words
-    against the oracle and status bits against the lane-group kernel (an
-    explicit lanes setting never takes phase 0) on the same frames."""
+    against the oracle on both variants, and status bits against the
+    sorted lane-group kernel on the same frames."""
     from roce_icrc import IcrcEngine
     import icrc_oracle as o  # checker only
     n = 64 * 300 + 17
@@ -215,7 +216,7 @@ def test_compact_batches_malformed_and_options(engine):
     np.testing.assert_array_equal(st_s, st)
     e8 = IcrcEngine(0, lanes=8)
     try:
-        got8, st8 = _dev_compute(e8, buf, offs, lens)
+        got8, st8 = _dev_compute(e8, buf, offs, lens, E.RAGGED_SORTED)
     finally:
         e8.close()
     np.testing.assert_array_equal(got8, want)
@@ -224,10 +225,11 @@ def test_compact_batches_malformed_and_options(engine):
 
 
 def test_compact_test_rejects_unsafe_layouts(engine):
-    """Batches phase 0 must NOT take (they go through the sort, still exact):
-    frames in reverse order, the same frame twice (in-place masks would be
-    applied twice), a gap that stretches the span past 4 KiB, frames at
-    2-byte offsets, and frames longer than 128 B between tiny ones."""
+    """Groups the compact test must NOT take (the compact kernel folds them by
+    lane groups, still exact): frames in reverse order, the same frame twice
+    (in-place masks would be applied twice), a gap that stretches the span
+    past 4 KiB, frames at 2-byte offsets, and frames longer than 128 B
+    between tiny ones -- on both variants."""
     rng = np.random.default_rng(8)
     n = 64 * 64
     lens = np.full(n, 48, np.uint32)
@@ -261,13 +263,12 @@ def test_compact_test_rejects_unsafe_layouts(engine):
 
 
 def test_compact_rounds_between_sorted_rounds(engine):
-    """Each wave folds the compact batches of its own descriptor rounds from
-    the lengths and span offsets of its test (icrc_kernels.hip,
-    compact_batches): 64-packet blocks that are all ACK-sized or all
-    longer frames, chosen per block, so a wave's compact and sorted rounds
-    interleave within a window; windows of compact rounds only; blocks
-    shifted by 32 packets (no round compact); a partial last window.
-    Compute and verify (flipped frames fail) against the oracle."""
+    """64-packet blocks that are all ACK-sized or all longer frames, chosen
+    per block: the compact kernel's waves alternate between compact groups
+    and lane-group fallback groups with their spans in flight across both
+    (and the sorted kernel sorts the same windows); runs of compact groups
+    only; blocks shifted by 32 packets (no group compact); a partial last
+    group.  Compute and verify (flipped frames fail) against the oracle."""
     rng = np.random.default_rng(31)
     for n, shift, p_ack in ((8192 * 40 + 777, 0, 0.5), (8192 * 24 + 64 * 5, 0, 0.97),
                             (8192 * 12 + 100, 32, 0.5)):
@@ -310,10 +311,11 @@ def test_bench_ack_workload_line():
 
 
 def test_kernel_choice_follows_the_frames():
-    """A fresh context: its first ragged launch runs the kernel without phase 0
-    (no hint yet); after tiny frames the next runs the one with it, after a
-    batch without tiny frames the next runs without it again -- every word
-    bit-exact either way (cfg3-shaped frames, ACK frames, alternating)."""
+    """AUTO on device-resident batches: a fresh context's first ragged launch
+    runs the sorted kernel (no hint yet); after ACK frames the next runs the
+    compact one, after a batch without tiny frames the next runs the sorted
+    one again -- every word bit-exact either way (cfg3-shaped frames, ACK
+    frames, alternating)."""
     torch = pytest.importorskip("torch")
     from roce_icrc import IcrcEngine, synth
     eng = IcrcEngine(0)
