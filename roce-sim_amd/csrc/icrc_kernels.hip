@@ -1098,16 +1098,25 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // and folds its frame there (four Mul(128) chains, three Mul(-32) steps, as
 // the window kernel's phase 0).  The pipeline per wave, two register sets
 // ping-ponging: while group i folds, the spans of groups i+1 and i+2 and the
-// descriptors of group i+3 are in flight -- eight KiB per wave, 128 KiB per
-// CU, against phase 0's one span per wave and a descriptor round trip plus
-// three barriers per 8192-packet window.  A group that fails the test
-// (frames out of order, overlapping, larger, unaligned) is folded in place
-// by G = 8 lane groups, eight packets at a time, out of line
-// (compact_fallback_group).
-constexpr int kCompactWaves = 12;
+// descriptors of group i+3 are in flight -- eight KiB per wave, against the
+// round-4 phase 0's one span per wave and a descriptor round trip plus three
+// barriers per 8192-packet window.  A group that fails the test (frames out
+// of order, overlapping, larger, unaligned) is listed in LDS and folded after
+// the pipeline has drained, by G = 8 lane groups, eight packets at a time
+// (compact_fallback_group): the pipeline's registers and the fallback's do
+// not overlap.  A workgroup's range goes in chunks of kCompactChunk groups
+// (the list's capacity).
+#ifndef RICRC_COMPACT_WAVES
+#define RICRC_COMPACT_WAVES 16
+#endif
+constexpr int kCompactWaves = RICRC_COMPACT_WAVES;
 constexpr int kCompactThreads = 64 * kCompactWaves;
 constexpr uint32_t kCompactSlots = kMixedLut + 256u;  // a kCompactSpan slot per wave
-static_assert(kCompactSlots + kCompactWaves * kCompactSpan <= 163840u, "compact kernel LDS");
+constexpr uint32_t kCompactChunk = 1024;               // groups per chunk: the deferred list's capacity
+constexpr uint32_t kCompactDefer = kCompactSlots + kCompactWaves * kCompactSpan;  // u32 x kCompactChunk
+constexpr uint32_t kCompactDeferN = kCompactDefer + 4u * kCompactChunk;           // two u32 counters
+constexpr size_t kCompactLdsBytes = kCompactDeferN + 8u;
+static_assert(kCompactLdsBytes <= 163840u, "compact kernel LDS");
 
 // One group of a wave after its test.  Per lane: descriptor, offset in the
 // span; uniform: the span's start (from the 16-byte line below frames) and
@@ -1158,18 +1167,11 @@ __device__ __forceinline__ CGroup compact_test(const IcrcArgs& a, uint32_t g, ui
 
 // A group that is not compact: eight sets of eight packets, G = 8 lanes per
 // packet (the window kernel's long-frame path, unsorted), Mul(1024) from the
-// table rows' low halves.  Out of line: the compact loop's registers stay its
-// own.
+// table rows' low halves.  L, off: the lane's descriptor (packet 64 g + lane).
 template <bool VERIFY>
-__device__ __noinline__ void compact_fallback_group(const uint8_t* frames, uint32_t n, uint32_t* icrc_out,
-                                                    uint8_t* status_out, uint8_t* ok_out, uint32_t g,
-                                                    uint32_t L, uint64_t off) {
-  IcrcArgs a{};
-  a.frames = frames;
-  a.n = n;
-  a.icrc_out = icrc_out;
-  a.status_out = status_out;
-  a.ok_out = ok_out;
+__device__ __forceinline__ void compact_fallback_group(const IcrcArgs& a, uint32_t g, uint32_t L, uint64_t off) {
+  const uint8_t* frames = a.frames;
+  const uint32_t n = a.n;
   const int lane = __lane_id();
   const int gl = lane & 7, grp = lane >> 3;
   const MixedKeysL kk = MixedKeysL::make(lane);
@@ -1199,6 +1201,9 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
   MixedKeysS::template stage<kCompactThreads>(a.tables + 0 * 1024, tid);
   // (uniform) the AUTO hint; scratch: the staging slots, not yet in use
   if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kCompactWaves>(a.tiny_hint, kCompactSlots, tid, probe);
+  lds_u32* const ndef = (lds_u32*)(uintptr_t)kCompactDeferN;  // deferred groups of chunk k: ndef[k & 1]
+  lds_u32* const defer = (lds_u32*)(uintptr_t)kCompactDefer;
+  if (tid < 2) ndef[tid] = 0;
   __syncthreads();
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1209,11 +1214,15 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
   const uint32_t per_block = (ngroups + gridDim.x - 1) / gridDim.x;
   const uint32_t g0 = blockIdx.x * per_block;
   const uint32_t g1 = min(ngroups, g0 + per_block);
-  // this wave's groups: g0 + wave + kCompactWaves i, i < cnt
-  const uint32_t first = g0 + (uint32_t)wave;
-  const int cnt = first < g1 ? (int)((g1 - first + kCompactWaves - 1) / kCompactWaves) : 0;
-  if (cnt == 0) return;
+  uint32_t chunk = 0;
+  for (uint32_t c0 = g0; c0 < g1; c0 += kCompactChunk, ++chunk) {
+  const uint32_t c1 = min(g1, c0 + kCompactChunk);
+  lds_u32* const nd = ndef + (chunk & 1u);
+  // this wave's groups of the chunk: c0 + wave + kCompactWaves i, i < cnt
+  const uint32_t first = c0 + (uint32_t)wave;
+  const int cnt = first < c1 ? (int)((c1 - first + kCompactWaves - 1) / kCompactWaves) : 0;
   auto group = [&](int i) { return first + (uint32_t)i * kCompactWaves; };
+  if (cnt > 0) {  // (uniform)
   // descriptors of the wave's group i (clamped: unconditional loads)
   auto load_desc = [&](int i, uint32_t& L, uint64_t& off) __attribute__((always_inline)) {
     const uint32_t gi = group(min(i, cnt - 1));
@@ -1230,12 +1239,12 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
 #pragma unroll
     for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
   };
-  // group i: patch, fold and emit from the slot (compact), or the fallback
+  // group i: patch, fold and emit from the slot (compact), or list it for
+  // the fallback after the chunk's pipeline
   auto run = [&](int i, const CGroup& c) __attribute__((always_inline)) {
     const uint32_t gi = group(i);
     if (c.span == 0) {  // (uniform)
-      compact_fallback_group<VERIFY>(a.frames, a.n, (OUTS & 1) ? a.icrc_out : nullptr,
-                                     (OUTS & 2) ? a.status_out : nullptr, a.ok_out, gi, c.L, c.off);
+      if (lane == 0) defer[atomicAdd((uint32_t*)nd, 1u)] = gi;
       return;
     }
     // (an opaque lane id: the compiler otherwise hoists the output addresses
@@ -1356,6 +1365,19 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
     step(i + 1, cb, XB, Lb, ob, La, oa);
   }
   if (i < cnt) step(i, ca, XA, La, oa, Lb, ob);
+  }  // (cnt > 0)
+  // the chunk's listed groups, by every wave of the workgroup; the other
+  // counter is free until the next chunk
+  __syncthreads();
+  const uint32_t ndc = (uint32_t)__builtin_amdgcn_readfirstlane((int)*nd);
+  if (tid == 0) ndef[(chunk + 1u) & 1u] = 0;
+  for (uint32_t k = (uint32_t)wave; k < ndc; k += kCompactWaves) {
+    const uint32_t gi = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer[k]);
+    const uint32_t p = min(gi * 64u + (uint32_t)lane, a.n - 1u);
+    compact_fallback_group<VERIFY>(a, gi, a.lens[p], a.offsets[p]);
+  }
+  __syncthreads();  // (the list is refilled by the next chunk)
+  }  // chunks
 }
 
 // ---------------------------------------------------------------------------
@@ -2172,7 +2194,6 @@ kernel_fn pick_compact(int outs) {
 kernel_fn select_compact(bool verify, int outs) {
   return verify ? pick_compact<true>(outs) : pick_compact<false>(outs);
 }
-constexpr size_t kCompactLdsBytes = kCompactSlots + kCompactWaves * kCompactSpan;
 
 size_t lds_bytes(int log2g, bool ragged) {
   if (!ragged) return 163840u;  // tables, fix-up LUT, then the block's ICRC words
