@@ -1107,7 +1107,10 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // not overlap.  A workgroup's range goes in chunks of kCompactChunk groups
 // (the list's capacity).
 #ifndef RICRC_COMPACT_WAVES
-#define RICRC_COMPACT_WAVES 16
+#define RICRC_COMPACT_WAVES 12
+#endif
+#ifndef RICRC_COMPACT_BUFS
+#define RICRC_COMPACT_BUFS 2
 #endif
 constexpr int kCompactWaves = RICRC_COMPACT_WAVES;
 constexpr int kCompactThreads = 64 * kCompactWaves;
@@ -1329,6 +1332,51 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
     __asm__ __volatile__("" ::: "memory");
   };
 
+#if RICRC_COMPACT_BUFS == 3
+  // Three span buffers: step i stages group i (its span issued three steps
+  // before), issues group i + 5's descriptors, tests group i + 3 (its
+  // descriptors issued two steps before, ahead of group i + 1's span: the
+  // wait for them retires no span still in flight), issues its span and
+  // folds group i -- spans i+1 .. i+3 in flight during the fold.  Buffer k
+  // holds the groups i = k mod 3; descriptor set k those i = k mod 3 as well.
+  uint32_t Ld[3], Lp0, Lp1, Lp2;
+  uint64_t od[3], op0, op1, op2;
+  load_desc(0, Lp0, op0);
+  load_desc(1, Lp1, op1);
+  load_desc(2, Lp2, op2);
+  load_desc(3, Ld[0], od[0]);
+  u32x4 X0[kCompactLoads], X1[kCompactLoads], X2[kCompactLoads];
+  CGroup c0 = compact_test(a, group(0), Lp0, op0, lane);
+  issue(c0, X0);
+  load_desc(4, Ld[1], od[1]);
+  CGroup c1 = compact_test(a, group(min(1, cnt - 1)), Lp1, op1, lane);
+  if (cnt < 2) c1.span = 0;
+  issue(c1, X1);
+  CGroup c2 = compact_test(a, group(min(2, cnt - 1)), Lp2, op2, lane);
+  if (cnt < 3) c2.span = 0;
+  issue(c2, X2);
+  auto step3 = [&](int i, CGroup& c, u32x4 (&X)[kCompactLoads], uint32_t& Lt, uint64_t& ot, uint32_t& Ln,
+                   uint64_t& on) __attribute__((always_inline)) {
+    const CGroup cur = c;
+    body_prio_hi();
+    if (cur.span != 0) stage(cur, X);  // (uniform)
+    load_desc(i + 5, Ln, on);
+    c = compact_test(a, group(min(i + 3, cnt - 1)), Lt, ot, lane);
+    if (i + 3 >= cnt) c.span = 0;
+    issue(c, X);
+    body_prio_lo();
+    run(i, cur);
+  };
+  // step i: group i + 3's descriptors in set i mod 3, group i + 5's into set (i + 2) mod 3
+  int i = 0;
+  for (; i + 2 < cnt; i += 3) {
+    step3(i, c0, X0, Ld[0], od[0], Ld[2], od[2]);
+    step3(i + 1, c1, X1, Ld[1], od[1], Ld[0], od[0]);
+    step3(i + 2, c2, X2, Ld[2], od[2], Ld[1], od[1]);
+  }
+  if (i < cnt) step3(i, c0, X0, Ld[0], od[0], Ld[2], od[2]);
+  if (i + 1 < cnt) step3(i + 1, c1, X1, Ld[1], od[1], Ld[0], od[0]);
+#else
   // Issue order, so that no wait retires a younger span: step i stages group
   // i (its span issued two steps before), issues group i + 3's descriptors,
   // tests group i + 2 (descriptors issued one step before, ahead of group
@@ -1365,6 +1413,7 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
     step(i + 1, cb, XB, Lb, ob, La, oa);
   }
   if (i < cnt) step(i, ca, XA, La, oa, Lb, ob);
+#endif
   }  // (cnt > 0)
   // the chunk's listed groups, by every wave of the workgroup; the other
   // counter is free until the next chunk
