@@ -1106,13 +1106,9 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // (compact_fallback_group): the pipeline's registers and the fallback's do
 // not overlap.  A workgroup's range goes in chunks of kCompactChunk groups
 // (the list's capacity).
-#ifndef RICRC_COMPACT_WAVES
-#define RICRC_COMPACT_WAVES 12
-#endif
-#ifndef RICRC_COMPACT_BUFS
-#define RICRC_COMPACT_BUFS 2
-#endif
-constexpr int kCompactWaves = RICRC_COMPACT_WAVES;
+// Twelve waves (A/B, round 5: 16 waves, or three span buffers per wave, ran
+// 2-4 % slower; at 16 waves the pipeline and the fallback's registers spill).
+constexpr int kCompactWaves = 12;
 constexpr int kCompactThreads = 64 * kCompactWaves;
 constexpr uint32_t kCompactSlots = kMixedLut + 256u;  // a kCompactSpan slot per wave
 constexpr uint32_t kCompactChunk = 1024;               // groups per chunk: the deferred list's capacity
@@ -1219,213 +1215,167 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
   const uint32_t g1 = min(ngroups, g0 + per_block);
   uint32_t chunk = 0;
   for (uint32_t c0 = g0; c0 < g1; c0 += kCompactChunk, ++chunk) {
-  const uint32_t c1 = min(g1, c0 + kCompactChunk);
-  lds_u32* const nd = ndef + (chunk & 1u);
-  // this wave's groups of the chunk: c0 + wave + kCompactWaves i, i < cnt
-  const uint32_t first = c0 + (uint32_t)wave;
-  const int cnt = first < c1 ? (int)((c1 - first + kCompactWaves - 1) / kCompactWaves) : 0;
-  auto group = [&](int i) { return first + (uint32_t)i * kCompactWaves; };
-  if (cnt > 0) {  // (uniform)
-  // descriptors of the wave's group i (clamped: unconditional loads)
-  auto load_desc = [&](int i, uint32_t& L, uint64_t& off) __attribute__((always_inline)) {
-    const uint32_t gi = group(min(i, cnt - 1));
-    const uint32_t p = min(gi * 64u + (uint32_t)lane, a.n - 1u);
-    L = a.lens[p];
-    off = a.offsets[p];
-  };
-  // a compact group's span chunks (unconditional, clamped); a group that is
-  // not compact loads 16 bytes of the table image (always mapped, L2-hot)
-  auto issue = [&](const CGroup& c, u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
-    const bool cp = c.span != 0;
-    const uint8_t* base = cp ? a.frames + (c.b16 - a.frames_lo4) : (const uint8_t*)a.tables;
-    const uint32_t last = cp ? (c.span + 15u) / 16u - 1u : 0u;
+    const uint32_t c1 = min(g1, c0 + kCompactChunk);
+    lds_u32* const nd = ndef + (chunk & 1u);
+    // this wave's groups of the chunk: c0 + wave + kCompactWaves i, i < cnt
+    const uint32_t first = c0 + (uint32_t)wave;
+    const int cnt = first < c1 ? (int)((c1 - first + kCompactWaves - 1) / kCompactWaves) : 0;
+    auto group = [&](int i) { return first + (uint32_t)i * kCompactWaves; };
+    if (cnt > 0) {  // (uniform)
+      // descriptors of the wave's group i (clamped: unconditional loads)
+      auto load_desc = [&](int i, uint32_t& L, uint64_t& off) __attribute__((always_inline)) {
+        const uint32_t gi = group(min(i, cnt - 1));
+        const uint32_t p = min(gi * 64u + (uint32_t)lane, a.n - 1u);
+        L = a.lens[p];
+        off = a.offsets[p];
+      };
+      // a compact group's span chunks (unconditional, clamped); a group that is
+      // not compact loads 16 bytes of the table image (always mapped, L2-hot)
+      auto issue = [&](const CGroup& c, u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
+        const bool cp = c.span != 0;
+        const uint8_t* base = cp ? a.frames + (c.b16 - a.frames_lo4) : (const uint8_t*)a.tables;
+        const uint32_t last = cp ? (c.span + 15u) / 16u - 1u : 0u;
 #pragma unroll
-    for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
-  };
-  // group i: patch, fold and emit from the slot (compact), or list it for
-  // the fallback after the chunk's pipeline
-  auto run = [&](int i, const CGroup& c) __attribute__((always_inline)) {
-    const uint32_t gi = group(i);
-    if (c.span == 0) {  // (uniform)
-      if (lane == 0) defer[atomicAdd((uint32_t*)nd, 1u)] = gi;
-      return;
-    }
-    // (an opaque lane id: the compiler otherwise hoists the output addresses
-    // of both unrolled groups)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint32_t pkt = gi * 64u + (uint32_t)ln;
-    const bool live = pkt < a.n;
-    const uint32_t L = c.L;  // (dead lanes repeat the last live frame)
-    const uint32_t pb = slot + c.rel;
-    const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the test checked every lane)
-    const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
-    const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
-    uint32_t st = 0;
-    const int ihl = (int)(d0 & 0xFu);
-    if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
-      st |= kPktNotIpv4;
-    else if (((d2 >> 8) & 0xFFu) != 17u)
-      st |= kPktNotUdp;
-    else if (L < (uint32_t)(4 * ihl + 24))
-      st |= kPktBadLen;
-    if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
-    const bool good = (st & kPktFatal) == 0;
-    uint32_t R;
-    if (__all(good && ihl == 5)) {
-      // masks and seed patched in place (every lane reads its dwords before
-      // any writes them: a dead lane's copy of the last frame writes the same
-      // values), then the four chains with the lane's own zero pad in front
-      // (absorbing zeros into a zero register keeps it zero, so shorter
-      // frames just start later)
-      lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
-      lds_wr(pb + 8, d2 | 0xFFFF00FFu);
-      lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
-      lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
-      __asm__ __volatile__("" ::: "memory");
-      int nsm = (n + 3) >> 2;
-      const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
-      if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
-      }
-      const int ns = __builtin_amdgcn_readfirstlane(nsm);
-      const int pad = 4 * ns - n;
-      const uint32_t pz = pb - 4u * (uint32_t)pad;
-      uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
-        if (j < ns) {  // uniform
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            const int kp = 4 * j + cc;
-            const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
-            kk.absorb(P[cc], T[cc], kp >= pad ? w : 0u);
-          }
+        for (int t = 0; t < kCompactLoads; ++t) X[t] = ldg128(base + 16u * min((uint32_t)(lane + 64 * t), last));
+      };
+      // group i: patch, fold and emit from the slot (compact), or list it for
+      // the fallback after the chunk's pipeline
+      auto run = [&](int i, const CGroup& c) __attribute__((always_inline)) {
+        const uint32_t gi = group(i);
+        if (c.span == 0) {  // (uniform)
+          if (lane == 0) defer[atomicAdd((uint32_t*)nd, 1u)] = gi;
+          return;
         }
-      }
-      R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
-      R = mul_comb(R, kComb) ^ P[1] ^ T[1];
-      R = mul_comb(R, kComb) ^ P[0] ^ T[0];
-    } else {
-      R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
-    }
-    const uint32_t icrc = good ? ~R : 0u;
-    if (live) {
-      if constexpr (VERIFY) {
-        const bool ok = good && trailer == icrc;
-        if (good && !ok) st |= kPktIcrcMismatch;
-        stg8<kCompactStorePol>(a.ok_out + pkt, ok ? 1u : 0u);
-      }
-      if constexpr ((OUTS & 1) != 0) stg32<kCompactStorePol>(a.icrc_out + pkt, icrc);
-      if constexpr ((OUTS & 2) != 0) stg8<kCompactStorePol>(a.status_out + pkt, st);
-    }
-    __asm__ __volatile__("" ::: "memory");
-  };
-  // write a group's span registers into the slot (the slot's previous group
-  // is folded: LDS ops of a wave run in issue order)
-  auto stage = [&](const CGroup& c, const u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
-    const uint32_t last = (c.span + 15u) / 16u - 1u;
+        // (an opaque lane id: the compiler otherwise hoists the output addresses
+        // of both unrolled groups)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t pkt = gi * 64u + (uint32_t)ln;
+        const bool live = pkt < a.n;
+        const uint32_t L = c.L;  // (dead lanes repeat the last live frame)
+        const uint32_t pb = slot + c.rel;
+        const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the test checked every lane)
+        const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
+        const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
+        uint32_t st = 0;
+        const int ihl = (int)(d0 & 0xFu);
+        if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
+          st |= kPktNotIpv4;
+        else if (((d2 >> 8) & 0xFFu) != 17u)
+          st |= kPktNotUdp;
+        else if (L < (uint32_t)(4 * ihl + 24))
+          st |= kPktBadLen;
+        if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
+        const bool good = (st & kPktFatal) == 0;
+        uint32_t R;
+        if (__all(good && ihl == 5)) {
+          // masks and seed patched in place (every lane reads its dwords before
+          // any writes them: a dead lane's copy of the last frame writes the same
+          // values), then the four chains with the lane's own zero pad in front
+          // (absorbing zeros into a zero register keeps it zero, so shorter
+          // frames just start later)
+          lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+          lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+          lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+          lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+          __asm__ __volatile__("" ::: "memory");
+          int nsm = (n + 3) >> 2;
+          const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
+          if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
 #pragma unroll
-    for (int t = 0; t < kCompactLoads; ++t)
-      *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
-    __asm__ __volatile__("" ::: "memory");
-  };
+            for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+          }
+          const int ns = __builtin_amdgcn_readfirstlane(nsm);
+          const int pad = 4 * ns - n;
+          const uint32_t pz = pb - 4u * (uint32_t)pad;
+          uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
+            if (j < ns) {  // uniform
+#pragma unroll
+              for (int cc = 0; cc < 4; ++cc) {
+                const int kp = 4 * j + cc;
+                const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
+                kk.absorb(P[cc], T[cc], kp >= pad ? w : 0u);
+              }
+            }
+          }
+          R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
+          R = mul_comb(R, kComb) ^ P[1] ^ T[1];
+          R = mul_comb(R, kComb) ^ P[0] ^ T[0];
+        } else {
+          R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
+        }
+        const uint32_t icrc = good ? ~R : 0u;
+        if (live) {
+          if constexpr (VERIFY) {
+            const bool ok = good && trailer == icrc;
+            if (good && !ok) st |= kPktIcrcMismatch;
+            stg8<kCompactStorePol>(a.ok_out + pkt, ok ? 1u : 0u);
+          }
+          if constexpr ((OUTS & 1) != 0) stg32<kCompactStorePol>(a.icrc_out + pkt, icrc);
+          if constexpr ((OUTS & 2) != 0) stg8<kCompactStorePol>(a.status_out + pkt, st);
+        }
+        __asm__ __volatile__("" ::: "memory");
+      };
+      // write a group's span registers into the slot (the slot's previous group
+      // is folded: LDS ops of a wave run in issue order)
+      auto stage = [&](const CGroup& c, const u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
+        const uint32_t last = (c.span + 15u) / 16u - 1u;
+#pragma unroll
+        for (int t = 0; t < kCompactLoads; ++t)
+          *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
+        __asm__ __volatile__("" ::: "memory");
+      };
 
-#if RICRC_COMPACT_BUFS == 3
-  // Three span buffers: step i stages group i (its span issued three steps
-  // before), issues group i + 5's descriptors, tests group i + 3 (its
-  // descriptors issued two steps before, ahead of group i + 1's span: the
-  // wait for them retires no span still in flight), issues its span and
-  // folds group i -- spans i+1 .. i+3 in flight during the fold.  Buffer k
-  // holds the groups i = k mod 3; descriptor set k those i = k mod 3 as well.
-  uint32_t Ld[3], Lp0, Lp1, Lp2;
-  uint64_t od[3], op0, op1, op2;
-  load_desc(0, Lp0, op0);
-  load_desc(1, Lp1, op1);
-  load_desc(2, Lp2, op2);
-  load_desc(3, Ld[0], od[0]);
-  u32x4 X0[kCompactLoads], X1[kCompactLoads], X2[kCompactLoads];
-  CGroup c0 = compact_test(a, group(0), Lp0, op0, lane);
-  issue(c0, X0);
-  load_desc(4, Ld[1], od[1]);
-  CGroup c1 = compact_test(a, group(min(1, cnt - 1)), Lp1, op1, lane);
-  if (cnt < 2) c1.span = 0;
-  issue(c1, X1);
-  CGroup c2 = compact_test(a, group(min(2, cnt - 1)), Lp2, op2, lane);
-  if (cnt < 3) c2.span = 0;
-  issue(c2, X2);
-  auto step3 = [&](int i, CGroup& c, u32x4 (&X)[kCompactLoads], uint32_t& Lt, uint64_t& ot, uint32_t& Ln,
-                   uint64_t& on) __attribute__((always_inline)) {
-    const CGroup cur = c;
-    body_prio_hi();
-    if (cur.span != 0) stage(cur, X);  // (uniform)
-    load_desc(i + 5, Ln, on);
-    c = compact_test(a, group(min(i + 3, cnt - 1)), Lt, ot, lane);
-    if (i + 3 >= cnt) c.span = 0;
-    issue(c, X);
-    body_prio_lo();
-    run(i, cur);
-  };
-  // step i: group i + 3's descriptors in set i mod 3, group i + 5's into set (i + 2) mod 3
-  int i = 0;
-  for (; i + 2 < cnt; i += 3) {
-    step3(i, c0, X0, Ld[0], od[0], Ld[2], od[2]);
-    step3(i + 1, c1, X1, Ld[1], od[1], Ld[0], od[0]);
-    step3(i + 2, c2, X2, Ld[2], od[2], Ld[1], od[1]);
-  }
-  if (i < cnt) step3(i, c0, X0, Ld[0], od[0], Ld[2], od[2]);
-  if (i + 1 < cnt) step3(i + 1, c1, X1, Ld[1], od[1], Ld[0], od[0]);
-#else
-  // Issue order, so that no wait retires a younger span: step i stages group
-  // i (its span issued two steps before), issues group i + 3's descriptors,
-  // tests group i + 2 (descriptors issued one step before, ahead of group
-  // i + 1's span), issues its span and folds group i.  Descriptors of the
-  // groups two and three ahead ping-pong between (La, oa) and (Lb, ob).
-  uint32_t L0, L1, La, Lb;
-  uint64_t o0, o1, oa, ob;
-  load_desc(0, L0, o0);
-  load_desc(1, L1, o1);
-  load_desc(2, La, oa);
-  u32x4 XA[kCompactLoads], XB[kCompactLoads];
-  CGroup ca = compact_test(a, group(0), L0, o0, lane);
-  issue(ca, XA);
-  CGroup cb = compact_test(a, group(min(1, cnt - 1)), L1, o1, lane);
-  if (cnt < 2) cb.span = 0;
-  issue(cb, XB);
-  // group i in (c, X); the next group's descriptors into (Ln, on); group
-  // i + 2's in (Lt, ot)
-  auto step = [&](int i, CGroup& c, u32x4 (&X)[kCompactLoads], uint32_t& Lt, uint64_t& ot, uint32_t& Ln,
-                  uint64_t& on) __attribute__((always_inline)) {
-    const CGroup cur = c;
-    body_prio_hi();
-    if (cur.span != 0) stage(cur, X);  // (uniform)
-    load_desc(i + 3, Ln, on);
-    c = compact_test(a, group(min(i + 2, cnt - 1)), Lt, ot, lane);
-    if (i + 2 >= cnt) c.span = 0;
-    issue(c, X);
-    body_prio_lo();
-    run(i, cur);
-  };
-  int i = 0;
-  for (; i + 1 < cnt; i += 2) {
-    step(i, ca, XA, La, oa, Lb, ob);
-    step(i + 1, cb, XB, Lb, ob, La, oa);
-  }
-  if (i < cnt) step(i, ca, XA, La, oa, Lb, ob);
-#endif
-  }  // (cnt > 0)
-  // the chunk's listed groups, by every wave of the workgroup; the other
-  // counter is free until the next chunk
-  __syncthreads();
-  const uint32_t ndc = (uint32_t)__builtin_amdgcn_readfirstlane((int)*nd);
-  if (tid == 0) ndef[(chunk + 1u) & 1u] = 0;
-  for (uint32_t k = (uint32_t)wave; k < ndc; k += kCompactWaves) {
-    const uint32_t gi = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer[k]);
-    const uint32_t p = min(gi * 64u + (uint32_t)lane, a.n - 1u);
-    compact_fallback_group<VERIFY>(a, gi, a.lens[p], a.offsets[p]);
-  }
-  __syncthreads();  // (the list is refilled by the next chunk)
+      // Issue order, so that no wait retires a younger span: step i stages group
+      // i (its span issued two steps before), issues group i + 3's descriptors,
+      // tests group i + 2 (descriptors issued one step before, ahead of group
+      // i + 1's span), issues its span and folds group i.  Descriptors of the
+      // groups two and three ahead ping-pong between (La, oa) and (Lb, ob).
+      uint32_t L0, L1, La, Lb;
+      uint64_t o0, o1, oa, ob;
+      load_desc(0, L0, o0);
+      load_desc(1, L1, o1);
+      load_desc(2, La, oa);
+      u32x4 XA[kCompactLoads], XB[kCompactLoads];
+      CGroup ca = compact_test(a, group(0), L0, o0, lane);
+      issue(ca, XA);
+      CGroup cb = compact_test(a, group(min(1, cnt - 1)), L1, o1, lane);
+      if (cnt < 2) cb.span = 0;
+      issue(cb, XB);
+      // group i in (c, X); the next group's descriptors into (Ln, on); group
+      // i + 2's in (Lt, ot)
+      auto step = [&](int i, CGroup& c, u32x4 (&X)[kCompactLoads], uint32_t& Lt, uint64_t& ot, uint32_t& Ln,
+                      uint64_t& on) __attribute__((always_inline)) {
+        const CGroup cur = c;
+        body_prio_hi();
+        if (cur.span != 0) stage(cur, X);  // (uniform)
+        load_desc(i + 3, Ln, on);
+        c = compact_test(a, group(min(i + 2, cnt - 1)), Lt, ot, lane);
+        if (i + 2 >= cnt) c.span = 0;
+        issue(c, X);
+        body_prio_lo();
+        run(i, cur);
+      };
+      int i = 0;
+      for (; i + 1 < cnt; i += 2) {
+        step(i, ca, XA, La, oa, Lb, ob);
+        step(i + 1, cb, XB, Lb, ob, La, oa);
+      }
+      if (i < cnt) step(i, ca, XA, La, oa, Lb, ob);
+    }  // (cnt > 0)
+    // the chunk's listed groups, by every wave of the workgroup; the other
+    // counter is free until the next chunk
+    __syncthreads();
+    const uint32_t ndc = (uint32_t)__builtin_amdgcn_readfirstlane((int)*nd);
+    if (tid == 0) ndef[(chunk + 1u) & 1u] = 0;
+    for (uint32_t k = (uint32_t)wave; k < ndc; k += kCompactWaves) {
+      const uint32_t gi = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer[k]);
+      const uint32_t p = min(gi * 64u + (uint32_t)lane, a.n - 1u);
+      compact_fallback_group<VERIFY>(a, gi, a.lens[p], a.offsets[p]);
+    }
+    __syncthreads();  // (the list is refilled by the next chunk)
   }  // chunks
 }
 
