@@ -41,11 +41,11 @@ else
   # the STREAM-read kernel reads the whole frame buffer: covered bytes + 4 B per frame
   BUF=$(python3 -c "import json; d=json.load(open('$OUT/bench_$TAG.json')); c=d['config']; print((c['covered_bytes_per_gpu'] + 4 * c['packets_per_gpu']) // 16 * 16)")
   KN=::icrc_
-  # the ragged verify kernel without phase 0 (the compute launch in setup fills trailers)
-  [ "$WL" = cfg3 ] && KN="icrc_ragged_mixed_kernel<true, false>"
-  # the ragged compute kernel with phase 0 (a context's first ragged launch runs
-  # the one without; bench's check runs the verify form)
-  [ "$WL" = ack ] && KN="icrc_ragged_mixed_kernel<false, true>"
+  # the sorted ragged verify kernel (cfg3 has no tiny frame: AUTO picks SORTED)
+  [ "$WL" = cfg3 ] && KN="icrc_ragged_mixed_kernel<true>"
+  # the compact ragged compute kernel with the ICRC output only (bench sets
+  # RICRC_RAGGED_COMPACT; its checks run the verify form)
+  [ "$WL" = ack ] && KN="icrc_compact_kernel<false, 1>"
   # FETCH_SIZE factor measured on this workload's own access pattern (scripts/fetch_calib.py)
   CAL=""
   CF=$R/profiles/r03b_fetch_calibration/$WL.json
