@@ -1095,8 +1095,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // dword-aligned, in order without overlap, inside 4 KiB from the first
 // frame's 16-byte line); a compact group's span arrives with four coalesced
 // 16-byte loads per lane, goes to the wave's LDS slot, and each lane patches
-// and folds its frame there (four Mul(128) chains, three Mul(-32) steps, as
-// the window kernel's phase 0).  The pipeline per wave, two register sets
+// and folds its frame there (two Mul(64) chains and a Mul(-32) step,
+// kCompactChains).  The pipeline per wave, two register sets
 // ping-ponging: while group i folds, the spans of groups i+1 and i+2 and the
 // descriptors of group i+3 are in flight -- eight KiB per wave, against the
 // round-4 phase 0's one span per wave and a descriptor round trip plus three
@@ -1109,6 +1109,12 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // Twelve waves (A/B, round 5: 16 waves, or three span buffers per wave, ran
 // 2-4 % slower; at 16 waves the pipeline and the fallback's registers spill).
 constexpr int kCompactWaves = 12;
+// Chains per frame: two over Mul(64) (the small-frame kernel's set), one
+// Mul(-32) combine step: ACK kernel 0.1930 -> 0.1865 ms over 4 A/B rounds
+// against four over Mul(128) and three steps (52 vs 60 lookups per 48-B
+// frame, profiles/r05/ab_r05h.txt).
+constexpr int kCompactChains = 2;
+constexpr int kCompactFoldSet = kCompactChains == 4 ? 0 : kMul64Set;
 constexpr int kCompactThreads = 64 * kCompactWaves;
 constexpr uint32_t kCompactSlots = kMixedLut + 256u;  // a kCompactSpan slot per wave
 constexpr uint32_t kCompactChunk = 1024;               // groups per chunk: the deferred list's capacity
@@ -1192,12 +1198,12 @@ template <bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
   announce_batch(a.busy);
-  // the window kernel's tables in phase 0: Mul(1024) in the rows' low halves
-  // with its combine sets and fix-up LUT (fallback groups), Mul(128) in the
-  // high halves (compact groups)
+  // Mul(1024) in the rows' low halves with the combine sets and fix-up LUT
+  // (fallback groups, as the window kernel), the compact fold's Mul(64) in
+  // the high halves
   const uint32_t probe = blockIdx.x == 0 ? a.lens[min((uint32_t)tid, a.n - 1u)] : 0xFFFFFFFFu;
   stage_tables<3, kCompactThreads, MixedKeysL>(a.tables, tid);
-  MixedKeysS::template stage<kCompactThreads>(a.tables + 0 * 1024, tid);
+  MixedKeysS::template stage<kCompactThreads>(a.tables + kCompactFoldSet * 1024, tid);
   // (uniform) the AUTO hint; scratch: the staging slots, not yet in use
   if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kCompactWaves>(a.tiny_hint, kCompactSlots, tid, probe);
   lds_u32* const ndef = (lds_u32*)(uintptr_t)kCompactDeferN;  // deferred groups of chunk k: ndef[k & 1]
@@ -1279,32 +1285,35 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
           lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
           lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
           __asm__ __volatile__("" ::: "memory");
-          int nsm = (n + 3) >> 2;
+          constexpr int CH = kCompactChains;
+          int nsm = (n + CH - 1) / CH;
           const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
           if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
           }
           const int ns = __builtin_amdgcn_readfirstlane(nsm);
-          const int pad = 4 * ns - n;
+          const int pad = CH * ns - n;
           const uint32_t pz = pb - 4u * (uint32_t)pad;
-          uint32_t P[4] = {0, 0, 0, 0}, T[4] = {0, 0, 0, 0};
+          uint32_t P[CH], T[CH];
 #pragma unroll
-          for (int j = 0; j < (int)(kCompactMaxLen / 16u); ++j) {
+          for (int cc = 0; cc < CH; ++cc) P[cc] = T[cc] = 0;
+#pragma unroll
+          for (int j = 0; j < (int)(kCompactMaxLen / 4u) / CH; ++j) {
             if (j < ns) {  // uniform
 #pragma unroll
-              for (int cc = 0; cc < 4; ++cc) {
-                const int kp = 4 * j + cc;
+              for (int cc = 0; cc < CH; ++cc) {
+                const int kp = CH * j + cc;
                 const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
                 kk.absorb(P[cc], T[cc], kp >= pad ? w : 0u);
               }
             }
           }
-          R = mul_comb(P[3] ^ T[3], kComb) ^ P[2] ^ T[2];
-          R = mul_comb(R, kComb) ^ P[1] ^ T[1];
-          R = mul_comb(R, kComb) ^ P[0] ^ T[0];
+          R = P[CH - 1] ^ T[CH - 1];
+#pragma unroll
+          for (int cc = CH - 2; cc >= 0; --cc) R = mul_comb(R, kComb) ^ P[cc] ^ T[cc];
         } else {
-          R = fold_masked4<false, MixedKeysS, kComb>(nullptr, pb, ihl, n);
+          R = fold_masked4<false, MixedKeysS, kComb, kCompactChains>(nullptr, pb, ihl, n);
         }
         const uint32_t icrc = good ? ~R : 0u;
         if (live) {
