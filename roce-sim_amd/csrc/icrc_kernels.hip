@@ -45,6 +45,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace ricrc {
 
 namespace {
@@ -1274,27 +1276,14 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
         if ((((d0 >> 8) & 0xFF00u) | (d0 >> 24)) != L) st |= kPktLenMismatch;
         const bool good = (st & kPktFatal) == 0;
         uint32_t R;
-        if (__all(good && ihl == 5)) {
-          // masks and seed patched in place (every lane reads its dwords before
-          // any writes them: a dead lane's copy of the last frame writes the same
-          // values), then the four chains with the lane's own zero pad in front
-          // (absorbing zeros into a zero register keeps it zero, so shorter
-          // frames just start later)
-          lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
-          lds_wr(pb + 8, d2 | 0xFFFF00FFu);
-          lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
-          lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
-          __asm__ __volatile__("" ::: "memory");
-          constexpr int CH = kCompactChains;
-          int nsm = (n + CH - 1) / CH;
-          const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
-          if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
-          }
-          const int ns = __builtin_amdgcn_readfirstlane(nsm);
-          const int pad = CH * ns - n;
-          const uint32_t pz = pb - 4u * (uint32_t)pad;
+        constexpr int CH = kCompactChains;
+        // the chains' fold from the slot with the lane's zero pad in front
+        // (absorbing zeros into a zero register keeps it zero, so shorter
+        // frames just start later); PAD < 0: per-lane pads, frames patched in
+        // place; else every frame of the group has the same length, its masks
+        // and seed applied in registers (dwords 0 and 2 are d0 and d2)
+        auto fold = [&](auto padc, int ns, uint32_t pz, int pad) __attribute__((always_inline)) {
+          constexpr int PAD = decltype(padc)::value;
           uint32_t P[CH], T[CH];
 #pragma unroll
           for (int cc = 0; cc < CH; ++cc) P[cc] = T[cc] = 0;
@@ -1304,14 +1293,58 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
 #pragma unroll
               for (int cc = 0; cc < CH; ++cc) {
                 const int kp = CH * j + cc;
-                const uint32_t w = lds_rd(pz + 4u * (uint32_t)kp);
-                kk.absorb(P[cc], T[cc], kp >= pad ? w : 0u);
+                uint32_t w;
+                if constexpr (PAD < 0) {
+                  w = lds_rd(pz + 4u * (uint32_t)kp);
+                  w = kp >= pad ? w : 0u;
+                } else {
+                  const int k = kp - PAD;  // (a constant after unrolling)
+                  if (k < 0)
+                    w = 0u;
+                  else if (k == 0)
+                    w = (d0 | 0x0000FF00u) ^ kSeedRegister;
+                  else if (k == 2)
+                    w = d2 | 0xFFFF00FFu;
+                  else
+                    w = lds_rd(pz + 4u * (uint32_t)kp);
+                  if (k == 6) w |= 0xFFFF0000u;
+                  if (k == 8) w |= 0x000000FFu;
+                }
+                kk.absorb(P[cc], T[cc], w);
               }
             }
           }
-          R = P[CH - 1] ^ T[CH - 1];
+          uint32_t r = P[CH - 1] ^ T[CH - 1];
 #pragma unroll
-          for (int cc = CH - 2; cc >= 0; --cc) R = mul_comb(R, kComb) ^ P[cc] ^ T[cc];
+          for (int cc = CH - 2; cc >= 0; --cc) r = mul_comb(r, kComb) ^ P[cc] ^ T[cc];
+          return r;
+        };
+        const int n0 = __builtin_amdgcn_readfirstlane(n);
+        if (__all(good && ihl == 5 && n == n0)) {  // (uniform) one length
+          const int ns = (n0 + CH - 1) / CH, pad = CH * ns - n0;
+          static_assert(CH == 2, "one instantiation per pad");
+          if (pad == 0)
+            R = fold(std::integral_constant<int, 0>{}, ns, pb, 0);
+          else
+            R = fold(std::integral_constant<int, 1>{}, ns, pb - 4u, 1);
+        } else if (__all(good && ihl == 5)) {
+          // masks and seed patched in place (every lane reads its dwords before
+          // any writes them: a dead lane's copy of the last frame writes the same
+          // values)
+          lds_wr(pb, (d0 | 0x0000FF00u) ^ kSeedRegister);
+          lds_wr(pb + 8, d2 | 0xFFFF00FFu);
+          lds_wr(pb + 24, lds_rd(pb + 24) | 0xFFFF0000u);
+          lds_wr(pb + 32, lds_rd(pb + 32) | 0x000000FFu);
+          __asm__ __volatile__("" ::: "memory");
+          int nsm = (n + CH - 1) / CH;
+          const int ns0 = __builtin_amdgcn_readfirstlane(nsm);
+          if (!__all(nsm == ns0)) {  // (uniform) frames of several lengths: the longest
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) nsm = max(nsm, __shfl_xor(nsm, d, 64));
+          }
+          const int ns = __builtin_amdgcn_readfirstlane(nsm);
+          const int pad = CH * ns - n;
+          R = fold(std::integral_constant<int, -1>{}, ns, pb - 4u * (uint32_t)pad, pad);
         } else {
           R = fold_masked4<false, MixedKeysS, kComb, kCompactChains>(nullptr, pb, ihl, n);
         }
