@@ -1501,6 +1501,15 @@ constexpr int kSmallOutRounds = 64;  // output ring depth in rounds (0 = off)
 // wave draining the ring, with or without bursts aligned to a global clock,
 // 0.320-0.344.
 constexpr int kSmallOutPol = 16;
+// Ring rounds held in registers before the LDS ring: each lane keeps its word
+// of the first kSmallRegRounds rounds of a ring window in a vector register
+// (uniform dynamic index), so a flush writes kSmallRegRounds + the LDS ring's
+// rounds at once (larger write bursts into the read stream).
+#ifndef RICRC_SMALL_REG_ROUNDS
+#define RICRC_SMALL_REG_ROUNDS 16
+#endif
+constexpr int kSmallRegRounds = RICRC_SMALL_REG_ROUNDS;
+typedef uint32_t small_regring_t __attribute__((ext_vector_type(kSmallRegRounds > 0 ? kSmallRegRounds : 1)));
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(IcrcArgs a) {
@@ -1557,6 +1566,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   const uint32_t rounds_cap =
       kRing ? min((uint32_t)kSmallOutRounds, (kSmallHoleWords + (kSmallEnd - ring) / 4u) / (nw * 64u)) : 0u;
   uint32_t ring_base = 0;  // first packet of the ring's current window
+  constexpr int RR = kRing ? kSmallRegRounds : 0;  // the window's rounds in registers
+  small_regring_t W = {};
+  uint32_t in_ring = 0;  // the current round's index in the window
   auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer,
                   bool to_ring = false) {
     const bool good = (st & kPktFatal) == 0;
@@ -1568,9 +1580,12 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
         a.ok_out[pkt] = ok ? 1 : 0;
       }
       if constexpr ((OUTS & 1) != 0) {
-        if (kRing && to_ring)
-          lds_wr(small_ring_word(ring, pkt - ring_base), icrc);
-        else
+        if (kRing && to_ring) {
+          if (RR > 0 && in_ring < (uint32_t)RR)  // (uniform)
+            W[in_ring] = icrc;
+          else
+            lds_wr(small_ring_word(ring, pkt - ring_base - (uint32_t)RR * nw * 64u), icrc);
+        } else
           a.icrc_out[pkt] = icrc;
       }
       if constexpr ((OUTS & 2) != 0) a.status_out[pkt] = (uint8_t)st;
@@ -1697,9 +1712,12 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint32_t nrounds = (bs_end - b0 + nw - 1) / nw;
     load(b0 + (uint32_t)wave);
     ring_base = b0 * 64u;
-    uint32_t in_ring = 0;
+    in_ring = 0;
     auto flush = [&]() {
-      const uint32_t words = min(in_ring * nw, bs_end - ring_base / 64u) * 64u;
+      // rounds [0, RR) from the waves' registers, the rest from the LDS ring
+      const uint32_t rb0 = ring_base / 64u, lb0 = rb0 + (uint32_t)RR * nw;
+      const uint32_t words =
+          in_ring > (uint32_t)RR && bs_end > lb0 ? min((in_ring - (uint32_t)RR) * nw, bs_end - lb0) * 64u : 0u;
       // lgkmcnt(0): this wave's ring words are written.  The compiler-level
       // memory clobbers pin the ring's LDS accesses on their side of the
       // barrier (the barrier intrinsic alone is not a memory operation at IR
@@ -1708,7 +1726,13 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_s_barrier();
       __asm__ __volatile__("" ::: "memory");
-      const auto dst = out_rsrc(a.icrc_out + ring_base, 4u * words);
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        const uint32_t b = rb0 + (uint32_t)r * nw + (uint32_t)wave;
+        if ((uint32_t)r < in_ring && b < bs_end)  // (uniform)
+          stg32<kSmallOutPol>(a.icrc_out + b * 64u + (uint32_t)lane, W[r]);
+      }
+      const auto dst = out_rsrc(a.icrc_out + (size_t)lb0 * 64u, 4u * words);
       for (uint32_t i = (uint32_t)tid; i < words / 4u; i += blockDim.x)
         out_store128<kSmallOutPol>(*(const lds_u32x4*)(uintptr_t)small_ring_quad(ring, i), dst, 16u * i);
       __asm__ __volatile__("" ::: "memory");
@@ -1718,14 +1742,15 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       ring_base += in_ring * nw * 64u;
       in_ring = 0;
     };
+    const uint32_t window = rounds_cap + (uint32_t)RR;
     for (uint32_t r = 0; r < nrounds; r += 2) {
       uint32_t b = b0 + r * nw + (uint32_t)wave;
       stage_and_fold(b, b + kSmallAhead * nw, b < bs_end);
-      if (++in_ring == rounds_cap) flush();
+      if (++in_ring == window) flush();
       if (r + 1 < nrounds) {
         b += nw;
         stage_and_fold(b, b + kSmallAhead * nw, b < bs_end);
-        if (++in_ring == rounds_cap) flush();
+        if (++in_ring == window) flush();
       }
     }
     if (in_ring) flush();
