@@ -228,7 +228,8 @@ int ensure_pkts(ricrc_ctx* c, size_t n) {
 // Strided frames this small go to the lane-per-packet kernel (automatic lanes
 // only; an explicit lanes setting forces the lane-group kernels).
 bool use_small(const ricrc_ctx* c, uint64_t stride, uint32_t len) {
-  return c->lanes == 0 && stride <= ricrc::kSmallMaxStride && stride % 4 == 0 && len <= stride &&
+  return c->lanes == 0 && stride <= ricrc::kSmallMaxStride && stride >= ricrc::kSmallMinStride &&
+         stride % 4 == 0 && len <= stride &&
          len >= 4 && len % 4 == 0;  // (other lengths: the lane-group kernels' slow path)
 }
 

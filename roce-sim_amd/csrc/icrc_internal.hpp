@@ -67,6 +67,12 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
 // Strided frames of at most kSmallMaxStride bytes (stride a multiple of 4):
 // the lane-per-packet kernel with LDS-staged, coalesced loads.
 constexpr uint32_t kSmallMaxStride = 128;
+// Shortest stride it takes: a frame under 44 B (IPv4 + UDP + BTH + ICRC) is
+// unusable in every kernel, and strides below hold nothing else.  The kernel
+// is instantiated per chunk count ceil(stride / 16) (16-byte loads per lane
+// per 64-frame batch).
+constexpr uint32_t kSmallMinStride = 44;
+constexpr int kSmallMinChunks = (int)((kSmallMinStride + 15u) / 16u), kSmallMaxChunks = (int)(kSmallMaxStride / 16u);
 hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream);
 
 // Enqueues the STREAM-style read kernel (roofline denominator).

@@ -1504,11 +1504,13 @@ constexpr int kSmallOutPol = 16;
 // Ring rounds held in registers before the LDS ring: each lane keeps its word
 // of the first kSmallRegRounds rounds of a ring window in a vector register
 // (uniform dynamic index), so a flush writes kSmallRegRounds + the LDS ring's
-// rounds at once (larger write bursts into the read stream).
-#ifndef RICRC_SMALL_REG_ROUNDS
-#define RICRC_SMALL_REG_ROUNDS 16
-#endif
-constexpr int kSmallRegRounds = RICRC_SMALL_REG_ROUNDS;
+// rounds at once (larger write bursts into the read stream).  cfg5 kernel ms
+// over 4 A/B rounds (profiles/r05/ab_r05k.txt, ab_r05l.txt, ab_r05m.txt):
+// 16 rounds -2.3 % against none (8 -1.9 %; 32 slower: spills); with the
+// batch's exact chunk count and unmasked DMA / slot reads (below; 88 -> 25
+// SGPRs spilled into VGPR lanes, 12 fewer VGPRs) 24 rounds and then 28 fit:
+// 0.2962 -> 0.2917 ms (28), 0.2900 with the early first DMA.
+constexpr int kSmallRegRounds = 28;
 typedef uint32_t small_regring_t __attribute__((ext_vector_type(kSmallRegRounds > 0 ? kSmallRegRounds : 1)));
 
 template <int C, bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
@@ -1520,16 +1522,6 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   constexpr int CH = kSmallChains;
   const int n = dead ? 0 : (int)((L - 4) >> 2);  // covered dwords (uniform, <= 31)
   const int ns = (n + CH - 1) / CH, pad = CH * ns - n;  // steps, zero dwords in front (0 or 1)
-  {
-    const uint32_t* m64 = a.tables + kMul64Set * 1024;  // Mul(32 CH)
-    for (int i = tid; i < 2048; i += (int)blockDim.x) {  // 8 copies of 1024 words, 2 quads
-      const int w = i >> 1, h = i & 1;  // w = t * 256 + e
-      lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), m64[w]);
-    }
-    const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
-    for (int i = tid; i < 1024; i += (int)blockDim.x) lds_wr(kSmallComb + 4u * i, cm32[i]);
-  }
-  __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
   const SmallKeys kk = SmallKeys::make(lane);
   const uint32_t nchunk = 4 * S;  // 16-byte chunks per batch (<= 64 C)
@@ -1566,7 +1558,8 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   const uint32_t rounds_cap =
       kRing ? min((uint32_t)kSmallOutRounds, (kSmallHoleWords + (kSmallEnd - ring) / 4u) / (nw * 64u)) : 0u;
   uint32_t ring_base = 0;  // first packet of the ring's current window
-  constexpr int RR = kRing ? kSmallRegRounds : 0;  // the window's rounds in registers
+  // the window's rounds in registers (C = 8: 24, as 28 spill a VGPR there)
+  constexpr int RR = kRing ? (C >= 8 ? 24 : kSmallRegRounds) : 0;
   small_regring_t W = {};
   uint32_t in_ring = 0;  // the current round's index in the window
   auto emit = [&](uint32_t pkt, bool live, uint32_t st, uint32_t R, uint32_t trailer,
@@ -1637,18 +1630,70 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
       a.claims ? a.claims + (size_t)(a.epoch % kClaimSlots) * kMaxClaimBlocks : nullptr;
   if (claims && tid == 0) atomicExch(&claims[blockIdx.x], (unsigned long long)a.epoch << 32);
   uint32_t lim = bs_end > 0 ? bs_end - 1u : 0u;  // prefetch clamp (no clamp while claiming)
-  auto load = [&](uint32_t b) __attribute__((always_inline)) {  // unconditional: clamped batch index
-    const uint8_t* base = a.frames + (uint64_t)min(b, lim) * 64u * S;
+  auto load_at = [&](const uint8_t* base) __attribute__((always_inline)) {
     // LDS-DMA straight into the wave's slot: chunk lane + 64 t of the batch
     // lands at stage + 1024 t + 16 lane; lanes past the batch's last chunk
     // stay idle (the slot holds exactly the batch)
 #pragma unroll
     for (int t = 0; t < C; ++t)
-      if ((uint32_t)(lane + 64 * t) < nchunk)
+      if (t < C - 1 || (uint32_t)(lane + 64 * t) < nchunk)  // (C: exactly ceil(nchunk / 64))
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(base + 16u * (uint32_t)(lane + 64 * t)),
             (__attribute__((address_space(3))) void*)(uintptr_t)(stage + 1024u * (uint32_t)t), 16, 0, 2);
   };
+  auto load = [&](uint32_t b) __attribute__((always_inline)) {  // unconditional: clamped batch index
+    load_at(a.frames + (uint64_t)min(b, lim) * 64u * S);
+  };
+  // The tables: their words are loaded into registers first, then the wave's
+  // first batch goes out (its DMA in flight while the tables are written and
+  // the workgroup meets at the barrier), then vmcnt(C) -- the C younger DMA
+  // loads may still be in flight -- and the LDS writes.  Mul(64) as 8 copies
+  // of 1024 words (2 quads each; >= 512 threads, launch_icrc_small: at most
+  // 4 words per thread), Mul(-32) unreplicated (256 quads).
+  {
+    const uint32_t* m64 = a.tables + kMul64Set * 1024;       // Mul(32 CH)
+    const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
+    // Loads and LDS writes the compiler cannot see: it does not count the
+    // DMA loads, so it would wait for them too (vmcnt(0)) before the writes.
+    auto ldg_asm = [](const uint32_t* p) {
+      uint32_t v;
+      __asm__ __volatile__("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+      return v;
+    };
+    auto ldg4_asm = [](const uint32_t* p) {
+      u32x4 v;
+      __asm__ __volatile__("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+      return v;
+    };
+    auto ds_wr128 = [](uint32_t addr, u32x4 v) {
+      __asm__ __volatile__("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+    };
+    constexpr int kTw = 4;
+    uint32_t tw[kTw];
+#pragma unroll
+    for (int k = 0; k < kTw; ++k)  // (unconditional: clamped index)
+      tw[k] = ldg_asm(m64 + (min(tid + k * (int)blockDim.x, 2047) >> 1));
+    const u32x4 cw = ldg4_asm(cm32 + 4 * min(tid, 255));
+    // (no branch around the DMA, or the compiler waits for it with the table
+    // words: a workgroup without staged batches loads a clamped full batch,
+    // or with none in the launch (n <= 64) the table image, and never folds it)
+    load_at(last > 0 ? a.frames + (uint64_t)min(b0 + (uint32_t)wave, lim) * 64u * S
+                     : (const uint8_t*)a.tables);
+    __asm__ __volatile__("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | C);  // vmcnt(C): the table words are in
+    __asm__ __volatile__("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < kTw; ++k) {
+      const int i = tid + k * (int)blockDim.x, w = i >> 1, h = i & 1;  // w = t * 256 + e
+      if (i < 2048) ds_wr128((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), u32x4{tw[k], tw[k], tw[k], tw[k]});
+    }
+    if (tid < 256) ds_wr128(kSmallComb + 16u * (uint32_t)tid, cw);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the writes are done before the barrier
+    __asm__ __volatile__("" ::: "memory");
+  }
+  // (the barrier alone: __syncthreads' fence would wait for the DMA, vmcnt(0))
+  __builtin_amdgcn_s_barrier();
+  __asm__ __volatile__("" ::: "memory");
   // One batch: the slot's batch has landed; the wave reads its frames into
   // registers and at once refills the slot with the next batch (in flight
   // during the fold, its loads at raised wave priority), then checks the
@@ -1665,7 +1710,8 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint32_t pz = pb - 4u * (uint32_t)pad;  // dword k at pz + 4 (k + pad)
     uint32_t D[CH * kSmallMaxSteps];
 #pragma unroll
-    for (int kp = 0; kp < CH * kSmallMaxSteps; ++kp) D[kp] = kp < CH * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
+    for (int kp = 0; kp < CH * kSmallMaxSteps; ++kp)
+      D[kp] = kp <= 4 * (C - 1) || kp < CH * ns ? lds_rd(pz + 4u * (uint32_t)kp) : 0u;
     const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * n) : 0u;
     __asm__ __volatile__("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read
@@ -1710,7 +1756,6 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     // rounds the ring goes out.  LDS-only waits at the barriers: the
     // prefetched loads stay in flight across them.
     const uint32_t nrounds = (bs_end - b0 + nw - 1) / nw;
-    load(b0 + (uint32_t)wave);
     ring_base = b0 * 64u;
     in_ring = 0;
     auto flush = [&]() {
@@ -1757,7 +1802,6 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   } else if (b0 < bs_end) {  // (uniform) loads stay inside batches [0, last)
     const uint32_t first = b0 + (uint32_t)wave;
     const int cnt = first < bs_end ? (int)((bs_end - first + nw - 1) / nw) : 0;
-    load(first);
     uint32_t b = first;
     int i = 0;
     for (; i + 1 < cnt; i += 2, b += 2 * nw) {
@@ -1784,6 +1828,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     };
     uint32_t cur = claim();
     if (cur != ~0u) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // (an unused first DMA has landed)
       load(cur);
       for (;;) {  // the next claim's loads go out while this batch folds
         const uint32_t nxt = claim();
@@ -2285,9 +2330,15 @@ kernel_fn pick_small(int outs) {
 }
 
 kernel_fn select_small(int C, bool verify, int outs) {
-  if (C == 4) return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
-  if (C == 7) return verify ? pick_small<7, true>(outs) : pick_small<7, false>(outs);
-  return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
+  switch (C) {
+    case 3: return verify ? pick_small<3, true>(outs) : pick_small<3, false>(outs);
+    case 4: return verify ? pick_small<4, true>(outs) : pick_small<4, false>(outs);
+    case 5: return verify ? pick_small<5, true>(outs) : pick_small<5, false>(outs);
+    case 6: return verify ? pick_small<6, true>(outs) : pick_small<6, false>(outs);
+    case 7: return verify ? pick_small<7, true>(outs) : pick_small<7, false>(outs);
+    case 8: return verify ? pick_small<8, true>(outs) : pick_small<8, false>(outs);
+    default: return nullptr;
+  }
 }
 
 
@@ -2316,7 +2367,7 @@ hipError_t prepare_kernels() {
         hipError_t e = set_dynamic_lds((const void*)select_kernel(l, r, v), (int)lds_bytes(l, r));
         if (e != hipSuccess) return e;
       }
-  for (int c : {4, 7, 8})
+  for (int c = kSmallMinChunks; c <= kSmallMaxChunks; ++c)
     for (int v = 0; v < 2; ++v)
       for (int o = 0; o < 4; ++o) {
         hipError_t e = set_dynamic_lds((const void*)select_small(c, v, o), 163840);
@@ -2364,17 +2415,18 @@ hipError_t launch_icrc(const IcrcArgs& a, int log2g, bool ragged, bool verify, i
 
 hipError_t launch_icrc_small(const IcrcArgs& a, bool verify, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
-  if (a.stride > kSmallMaxStride || (a.stride & 3u) || a.stride == 0) return hipErrorInvalidValue;
-  // 16-byte loads per lane per batch (>= 4 * stride / 64).  C = 7 up to 112-B
-  // strides (cfg5, 108 B: 432 chunks): with C = 8 every lane's 8th load and
-  // LDS write were copies of the batch's last chunk (64 lanes writing one
-  // 16-byte LDS address)
-  const int C = a.stride <= 64 ? 4 : a.stride <= 112 ? 7 : 8;
+  if (a.stride > kSmallMaxStride || (a.stride & 3u) || a.stride < kSmallMinStride) return hipErrorInvalidValue;
+  // 16-byte loads per lane per batch: exactly ceil(4 stride / 64), so only
+  // the last one is partial (cfg5, 108 B: 432 chunks, C = 7)
+  const int C = (int)((a.stride + 15u) / 16u);
+  if (C < kSmallMinChunks || C > kSmallMaxChunks) return hipErrorInvalidValue;
   const int outs = (a.icrc_out ? 1 : 0) | (a.status_out ? 2 : 0);
   kernel_fn k = select_small(C, verify, outs);
+  if (!k) return hipErrorInvalidValue;
   const uint32_t slot = 64u * (uint32_t)a.stride;
   uint32_t nw = min((uint32_t)kSmallMaxWaves, (kSmallEnd - kSmallStage) / slot);
   if (nw > 2 && (nw & 1u)) --nw;  // even: every SIMD the same number of waves
+  if (nw < 8) return hipErrorInvalidValue;  // (the kernel stages its tables with >= 512 threads)
   const size_t lds = 163840;  // staging slots, then the output ring in what is left
   const uint64_t nb = (a.n + 63) / 64;
   uint64_t blocks = (nb + nw - 1) / nw;
