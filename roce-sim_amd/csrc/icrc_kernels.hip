@@ -804,6 +804,37 @@ template <bool GLOBAL, class K, uint32_t COMB, int CH = 4>
 __device__ __noinline__ uint32_t small_fold_masked(const uint8_t* f, uint32_t pb, int ihl, int n) {
   return fold_masked4<GLOBAL, K, COMB, CH>(f, pb, ihl, n);
 }
+// The same fold of a frame in global memory (n <= kSmallMaxStride / 4 - 1
+// covered dwords, any IHL): every dword is loaded first, so the frame costs
+// one memory round trip instead of one per step: the small-frame kernel's
+// last batch, at the very end of the launch (inline there: its registers are
+// free; the in-loop fallback for IPv4 options keeps the call above).
+template <class K, uint32_t COMB, int CH>
+__device__ __forceinline__ uint32_t small_fold_masked_global(const uint8_t* f, int ihl, int n) {
+  constexpr int KP = (int)(kSmallMaxStride / 4u);  // padded dwords kp = k + pad < KP
+  const K kk = K::make(__lane_id());
+  const int ns = (n + CH - 1) / CH, pad = CH * ns - n;
+  uint32_t D[KP];
+#pragma unroll
+  for (int kp = 0; kp < KP; ++kp) D[kp] = ldg32(f + 4 * max(min(kp - pad, n - 1), 0));
+  uint32_t P[CH], T[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) P[c] = T[c] = 0;
+#pragma unroll
+  for (int j = 0; j < KP / CH; ++j) {
+    if (j < ns) {  // uniform
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int kp = CH * j + c, k = kp - pad;
+        kk.absorb(P[c], T[c], k >= 0 ? fix_dword(D[kp], k, ihl + 1, ihl + 3) : 0u);
+      }
+    }
+  }
+  uint32_t R = P[CH - 1] ^ T[CH - 1];
+#pragma unroll
+  for (int c = CH - 2; c >= 0; --c) R = comb4<COMB>(R, kk) ^ P[c] ^ T[c];
+  return R;
+}
 
 // Compact groups (the ragged COMPACT variant, icrc_compact_kernel below): 64
 // consecutive packets whose frames (44-128 B, dword-aligned) lie in order,
@@ -1846,7 +1877,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
     int ihl;
     const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
-    const uint32_t R = small_fold_masked<true, SmallKeys, kSmallComb, CH>(f, 0u, ihl, n);
+    const uint32_t R = small_fold_masked_global<SmallKeys, kSmallComb, CH>(f, ihl, n);
     emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
   }
 }
