@@ -20,8 +20,9 @@ when fewer) and the line fails (exit status 3) on any mismatch.
 
 Printed (rank 0): ONE JSON line with the driver's keys plus
   roofline      -- achieved algorithmic GB/s of the ICRC kernel (per-launch
-                   bytes / mean launch time from HIP events on the launch
-                   stream) against the 8.0 TB/s HBM peak, and the PMC-measured
+                   bytes / mean launch time: the K back-to-back timed launches
+                   between one pair of HIP events on the launch stream, / K)
+                   against the 8.0 TB/s HBM peak, and the PMC-measured
                    HBM traffic per launch when profiles/pmc_traffic_<workload>.json holds
                    it for this workload AND for this very build (the file
                    records the sha256 of the libroceicrc.so it was measured
@@ -652,7 +653,7 @@ def enqueue_ceiling(torch, eng, W, stream, sp, dev):
     into the frame buffer (read + write bytes): a back-to-back series of
     >= CEIL_MIN_S, ENQUEUED without a final synchronisation so the warm-up
     steps follow it with no idle gap (see main()).  Returns a function that,
-    after the stream has been synchronised, gives (key, GB/s median, times)."""
+    after the stream has been synchronised, gives (key, GB/s, times)."""
     if isinstance(W, Segment):
         nb = W.mr.size // 16 * 16
         key, nbytes = "stream_copy_GBps", 2 * nb
@@ -672,16 +673,16 @@ def enqueue_ceiling(torch, eng, W, stream, sp, dev):
     launch()
     torch.cuda.synchronize(dev)
     k = int(min(400, max(20, CEIL_MIN_S / max(time.perf_counter() - t0, 1e-5))))
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(k)]
-    for a, b in evs:
-        a.record(stream)
+    # timed as the ICRC launches are: back to back between one pair of events
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(k):
         launch()
-        b.record(stream)
+    e1.record(stream)
 
     def result():
-        ts = [a.elapsed_time(b) * 1e-3 for a, b in evs]
-        return key, nbytes / float(np.median(ts)) / 1e9, ts
+        t = e0.elapsed_time(e1) * 1e-3 / k
+        return key, nbytes / t / 1e9, [t] * k
     return result
 
 
@@ -787,29 +788,45 @@ def main():
     # slower launches); coming straight from another HBM-saturating kernel
     # they do not dip (measured: profiles/r02_transient.txt).  The timed steps
     # are unchanged.
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    wev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.warmup)]
+    #
+    # The K timed launches go back to back between ONE pair of HIP events on
+    # the launch stream; the mean launch duration is their elapsed time / K
+    # (inter-launch gaps included).  An event pair around every launch -- the
+    # form up to round 5 -- costs ~6 us per step of wall time and ~1.5 us of
+    # every bracketed launch (cfg2 629.8 vs 622.9 us per step, cfg5 294.6 vs
+    # 289.4; profiles/r05/step_gap_r05.txt); ROCE_ICRC_BENCH_TRACE keeps that
+    # form for per-launch times.
+    trace = bool(os.environ.get("ROCE_ICRC_BENCH_TRACE"))
+    new_ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    evs = [(new_ev(), new_ev()) for _ in range(args.steps)] if trace else []
+    wev = [(new_ev(), new_ev()) for _ in range(args.warmup)] if trace else []
+    ev0, ev1 = new_ev(), new_ev()
     ceiling = enqueue_ceiling(torch, eng, W, stream, sp, dev)
-    for a, b in wev:
-        a.record(stream)
+    for i in range(args.warmup):
+        if trace:
+            wev[i][0].record(stream)
         W.step(sp)
-        b.record(stream)
+        if trace:
+            wev[i][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for a, b in evs:
-        a.record(stream)
+    ev0.record(stream)
+    for i in range(args.steps):
+        if trace:
+            evs[i][0].record(stream)
         W.step(sp)
-        b.record(stream)
+        if trace:
+            evs[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     t_local = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    kern_s = [a.elapsed_time(b) * 1e-3 for a, b in evs]
+    kern_s = ([a.elapsed_time(b) * 1e-3 for a, b in evs] if trace
+              else [ev0.elapsed_time(ev1) * 1e-3 / args.steps] * args.steps)
     # the ragged kernel variant the timed launches ran (the last launch's: the
     # variant is fixed per launch on the host, include/roce_icrc.h)
     ragged_kernel = None
@@ -817,7 +834,7 @@ def main():
         ragged_kernel = {1: "compact", 2: "sorted"}.get(
             eng.last_ragged_variant(), "none")
     ceil_key, ceil_gbps, ceil_ts = ceiling()
-    if os.environ.get("ROCE_ICRC_BENCH_TRACE"):  # per-launch times (us) to stderr
+    if trace:  # per-launch times (us) to stderr
         us = lambda xs: [round(x * 1e6) for x in xs]  # noqa: E731
         gap = wev[-1][1].elapsed_time(evs[0][0]) * 1e3 if wev and evs else -1.0
         print(f"[trace] rank {rank} ceiling n={len(ceil_ts)} {us(ceil_ts)}\n[trace] warmup "
