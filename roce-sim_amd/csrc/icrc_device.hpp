@@ -34,6 +34,10 @@ __device__ __forceinline__ void lds_wr4(uint32_t byte_addr, uint32_t v) {
 // before its first LDS write, so the copy costs one memory round trip.  (As
 // plain loops -- a guarded load, then the write -- the compiler waited for
 // each load in turn: a few microseconds of every launch's prologue.)
+// Every write is unconditional (a thread past COUNT writes word COUNT - 1
+// again, the same value): with a guarded write the compiler sank that load
+// into the guard, behind the waits for the other writes -- one more round
+// trip per table set.
 template <int COUNT, int THREADS, class Load, class Store>
 __device__ __forceinline__ void stage_batched(int tid, Load ld, Store st) {
   constexpr int R = (COUNT + THREADS - 1) / THREADS;
@@ -41,11 +45,28 @@ __device__ __forceinline__ void stage_batched(int tid, Load ld, Store st) {
 #pragma unroll
   for (int r = 0; r < R; ++r) v[r] = ld(min(tid + r * THREADS, COUNT - 1));
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int i = tid + r * THREADS;
-    if (COUNT % THREADS == 0 || i < COUNT) st(i, v[r]);
-  }
+  for (int r = 0; r < R; ++r) st(min(tid + r * THREADS, COUNT - 1), v[r]);
 }
+
+// stage_batched in two halves, for a prologue that issues other loads in
+// between: load() puts the thread's words in registers, store() writes them
+// to LDS later (the compiler then waits only for these loads, not for the
+// younger ones issued in between).
+template <int COUNT, int THREADS>
+struct StageRegs {
+  static constexpr int R = (COUNT + THREADS - 1) / THREADS;
+  uint32_t v[R];
+  template <class Load>
+  __device__ __forceinline__ void load(int tid, Load ld) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = ld(min(tid + r * THREADS, COUNT - 1));
+  }
+  template <class Store>
+  __device__ __forceinline__ void store(int tid, Store st) const {  // (unconditional: see stage_batched)
+#pragma unroll
+    for (int r = 0; r < R; ++r) st(min(tid + r * THREADS, COUNT - 1), v[r]);
+  }
+};
 
 __device__ __forceinline__ uint32_t ldg32(const uint8_t* p) {
   return *(const uint32_t*)p;
@@ -229,13 +250,24 @@ struct Keys32 {
   }
   template <int THREADS>
   __device__ static void stage(const uint32_t* m, int tid) {
-    stage_batched<8192, THREADS>(  // 8192 16-byte quads
-        tid, [&](int i) { return m[(i >> 11) * 256 + ((i >> 3) & 255)]; },
-        [&](int i, uint32_t v) {
-          const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
-          lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), v);
-        });
+    Staged<THREADS> st;
+    st.load(m, tid);
+    st.store(tid);
   }
+  // the same staging in two halves (StageRegs): 8192 16-byte quads
+  template <int THREADS>
+  struct Staged {
+    StageRegs<8192, THREADS> r;
+    __device__ __forceinline__ void load(const uint32_t* m, int tid) {
+      r.load(tid, [&](int i) { return m[(i >> 11) * 256 + ((i >> 3) & 255)]; });
+    }
+    __device__ __forceinline__ void store(int tid) const {
+      r.store(tid, [&](int i, uint32_t v) {
+        const int tab = i >> 11, e = (i >> 3) & 255, q = i & 7;
+        lds_wr4((uint32_t)((tab >> 1) * 65536 + e * 256 + (tab & 1) * 128 + q * 16), v);
+      });
+    }
+  };
   __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
     const uint32_t x = xor3(P, T, w);
     const uint32_t a0 = __builtin_amdgcn_perm(x, kc0, 0x0C0C0400u);
@@ -313,13 +345,25 @@ struct Keys8T {
   }
   template <int THREADS>
   __device__ static void stage(const uint32_t* m, int tid) {
-    stage_batched<2048, THREADS>(  // 1024 words x 2 quads of copies, w = t * 256 + e
-        tid, [&](int i) { return m[i >> 1]; },
-        [&](int i, uint32_t v) {
-          const int w = i >> 1, h = i & 1;
-          lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128 * HALF), v);
-        });
+    Staged<THREADS> st;
+    st.load(m, tid);
+    st.store(tid);
   }
+  // the same staging in two halves (StageRegs): 1024 words x 2 quads of
+  // copies, w = t * 256 + e
+  template <int THREADS>
+  struct Staged {
+    StageRegs<2048, THREADS> r;
+    __device__ __forceinline__ void load(const uint32_t* m, int tid) {
+      r.load(tid, [&](int i) { return m[i >> 1]; });
+    }
+    __device__ __forceinline__ void store(int tid) const {
+      r.store(tid, [&](int i, uint32_t v) {
+        const int w = i >> 1, h = i & 1;
+        lds_wr4((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16 + 128 * HALF), v);
+      });
+    }
+  };
   __device__ __forceinline__ void absorb(uint32_t& P, uint32_t& T, uint32_t w) const {
     const uint32_t x = xor3(P, T, w);
     const uint32_t a0 = __builtin_amdgcn_perm(x, k, s0);
@@ -369,14 +413,35 @@ __device__ __forceinline__ void fold_last(Col& c, const u32x4& w, int kb, int n,
 template <int LOG2G, class K>
 constexpr uint32_t kFixLut = K::kComb + 4096u * (1 + LOG2G);
 
-// LDS staging of the folding tables (every lane-group kernel, once per workgroup).
+// stage_tables (below) in two halves: load() the words, store() them (and
+// the fix-up LUT) later.
+template <int LOG2G, int THREADS, class K>
+struct TablesStaged {
+  static constexpr int NCOMB = 1 + LOG2G;
+  typename K::template Staged<THREADS> main;
+  StageRegs<NCOMB * 1024, THREADS> comb;
+  __device__ __forceinline__ void load(const uint32_t* tables, int tid) {
+    main.load(tables + LOG2G * 1024, tid);
+    const uint32_t* gc = tables + kNumMainSets * 1024;
+    comb.load(tid, [&](int i) { return gc[i]; });
+  }
+  __device__ __forceinline__ void store(int tid) const;
+};
+
+// LDS staging of the folding tables (every lane-group kernel, once per
+// workgroup): every word of the main set and the combine sets is loaded
+// first, one round trip, then written.
 template <int LOG2G, int THREADS, class K>
 __device__ __forceinline__ void stage_tables(const uint32_t* tables, int tid) {
-  constexpr int NCOMB = 1 + LOG2G;
-  K::template stage<THREADS>(tables + LOG2G * 1024, tid);
-  const uint32_t* gc = tables + kNumMainSets * 1024;
-  stage_batched<NCOMB * 1024, THREADS>(
-      tid, [&](int i) { return gc[i]; }, [&](int i, uint32_t v) { lds_wr(K::kComb + 4u * i, v); });
+  TablesStaged<LOG2G, THREADS, K> t;
+  t.load(tables, tid);
+  t.store(tid);
+}
+
+template <int LOG2G, int THREADS, class K>
+__device__ __forceinline__ void TablesStaged<LOG2G, THREADS, K>::store(int tid) const {
+  main.store(tid);
+  comb.store(tid, [&](int i, uint32_t v) { lds_wr(K::kComb + 4u * i, v); });
   if (tid < 13) {  // IHL-5 fix-up table, entry k + 3 (see fix_chunk5)
     const int k = tid - 3;
     const uint32_t lut = kFixLut<LOG2G, K>;

@@ -879,8 +879,14 @@ __device__ __forceinline__ void mixed_set(const IcrcArgs& a, int s, int e, uint3
 // The workgroup's windows.  (Round 4's compact tiny batches inside the
 // windows -- "phase 0" -- became a kernel of their own in round 5,
 // icrc_compact_kernel below.)
-template <bool VERIFY>
-__device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
+// Prologue: the first window's descriptors go out first, then the table
+// words (issue_tables), then the tables are written to LDS (write_tables):
+// one round trip for both instead of two in a row at the start of every
+// launch.  (Writing the tables only after the first window's keys are
+// counted kept their words live across the window loop: spilled.)
+template <bool VERIFY, class IssueTables, class WriteTables>
+__device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid, IssueTables issue_tables,
+                                              WriteTables write_tables) {
   constexpr int DPI = 32;  // sort key: G = 8 iterations
   using LD = MixedLds;
   constexpr int W = LD::kWindow;
@@ -929,6 +935,10 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
       Or[r] = __builtin_nondeterministic_value(Or[r]);
     }
   };
+  if (p0 < p1) load_descriptors(p0, (int)min(wsz, p1 - p0));  // (uniform) the first window's
+  issue_tables();
+  write_tables();
+  bool first = true;  // (uniform)
   for (uint32_t w0 = p0; w0 < p1; w0 += wsz) {
     const int cnt = (int)min(wsz, p1 - w0);
     if (tid < NB) hist[tid] = 0;
@@ -937,7 +947,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
     __syncthreads();
     int keys[KR];
     uint32_t offw[KR], lw[KR];  // (the sort runs outside the set loop: registers are free)
-    load_descriptors(w0, cnt);
+    if (!first) load_descriptors(w0, cnt);
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       const bool compact = false;  // (round 4: the packet of a compact batch)
@@ -964,6 +974,7 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid) {
       if (counted) atomicAdd((uint32_t*)&hist[keys[r]], 1u);
     }
     kill_descriptors();
+    first = false;
     __syncthreads();
     OutBuf ob = {0, 0};
     if constexpr (VERIFY) {
@@ -1109,11 +1120,20 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
   const uint32_t p1 = min(a.n, p0 + per_block);
   const uint32_t probe = blockIdx.x == 0 && p0 < p1 ? a.lens[p0 + min((uint32_t)tid, p1 - p0 - 1u)] : 0xFFFFFFFFu;
   announce_batch(a.busy);
-  stage_tables<3, kIcrcThreads, MixedKeysL>(a.tables, tid);
-  MixedKeysS::template stage<kIcrcThreads>(a.tables + 2 * 1024, tid);
   // (uniform) the hint; scratch: the window's sort arrays, not yet in use
   if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kIcrcWaves>(a.tiny_hint, MixedLds::kPerm, tid, probe);
-  mixed_windows<VERIFY>(a, tid);
+  TablesStaged<3, kIcrcThreads, MixedKeysL> tl;
+  MixedKeysS::Staged<kIcrcThreads> ts;
+  mixed_windows<VERIFY>(
+      a, tid,
+      [&]() __attribute__((always_inline)) {
+        tl.load(a.tables, tid);
+        ts.load(a.tables + 2 * 1024, tid);
+      },
+      [&]() __attribute__((always_inline)) {
+        tl.store(tid);
+        ts.store(tid);
+      });
 }
 
 // ---------------------------------------------------------------------------
@@ -1235,8 +1255,14 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
   // (fallback groups, as the window kernel), the compact fold's Mul(64) in
   // the high halves
   const uint32_t probe = blockIdx.x == 0 ? a.lens[min((uint32_t)tid, a.n - 1u)] : 0xFFFFFFFFu;
-  stage_tables<3, kCompactThreads, MixedKeysL>(a.tables, tid);
-  MixedKeysS::template stage<kCompactThreads>(a.tables + kCompactFoldSet * 1024, tid);
+  {  // both table sets' words first: one round trip
+    TablesStaged<3, kCompactThreads, MixedKeysL> tl;
+    MixedKeysS::Staged<kCompactThreads> ts;
+    tl.load(a.tables, tid);
+    ts.load(a.tables + kCompactFoldSet * 1024, tid);
+    tl.store(tid);
+    ts.store(tid);
+  }
   // (uniform) the AUTO hint; scratch: the staging slots, not yet in use
   if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kCompactWaves>(a.tiny_hint, kCompactSlots, tid, probe);
   lds_u32* const ndef = (lds_u32*)(uintptr_t)kCompactDeferN;  // deferred groups of chunk k: ndef[k & 1]
