@@ -85,8 +85,10 @@ int ricrc_device_count(int* count);
 int ricrc_ctx_create(int device, ricrc_ctx** out);
 void ricrc_ctx_destroy(ricrc_ctx* ctx);
 /* Lanes cooperating on one packet (1,2,4,...,64); 0 = automatic by length
- * (strided frames with stride <= 128 bytes, a multiple of 4, then use the
- * lane-per-packet kernel with LDS-staged loads; any non-zero setting forces
+ * (strided frames with a stride of 44-128 bytes, a multiple of 4, then use
+ * the lane-per-packet kernel with LDS-staged loads -- shorter strides hold
+ * only unusable frames, which the lane-group kernels mark RICRC_PKT_BAD_LEN
+ * as that kernel would; any non-zero setting forces
  * the lane-group kernels).  For ragged batches 8 selects the mixed-width
  * kernel, which runs sorted claims of short frames (<= 600 B) with 4 lanes
  * per packet and the rest with 8; it is also the automatic choice of the

@@ -8,7 +8,7 @@ import pytest
 
 import icrc_oracle as o
 from conftest import oracle_batch
-from roce_icrc.engine import PKT_ICRC_MISMATCH, PKT_NOT_IPV4
+from roce_icrc.engine import PKT_BAD_LEN, PKT_ICRC_MISMATCH, PKT_NOT_IPV4
 
 pytestmark = pytest.mark.gpu
 
@@ -163,3 +163,26 @@ def test_device_resident_options_and_malformed(engine, L):
     np.testing.assert_array_equal(got, want)
     bad = np.array([i % 31 == 5 for i in range(n)])
     assert (got[bad] == 0).all()
+
+
+@pytest.mark.parametrize("stride", [4, 32, 40, 44, 48])
+def test_strides_under_44_bytes(engine, stride):
+    """Strides under 44 B hold only unusable frames (shorter than IPv4 + UDP +
+    BTH + ICRC): they go to the lane-group kernels (the lane-per-packet kernel
+    is instantiated from ceil(stride / 16) = 3 chunks up), which give every
+    frame ICRC 0 and the bad-length status, as the oracle does (no ICRC); a
+    44-B stride is the lane-per-packet kernel's shortest."""
+    n = 1000
+    rng = np.random.default_rng(stride)
+    if stride >= 44:
+        buf = _strided(n, stride, stride, rng)
+        want, _ = oracle_batch(buf, stride=stride, length=stride, n=n)
+        assert engine.lanes_for_len(stride) == 1
+    else:
+        buf = rng.integers(0, 256, n * stride, dtype=np.uint8)
+        want = np.zeros(n, np.uint32)
+        assert engine.lanes_for_len(stride) > 1
+    got, st = engine.compute_strided(buf, stride, stride, n)
+    np.testing.assert_array_equal(got, want)
+    if stride < 44:
+        assert (st == PKT_BAD_LEN).all()
