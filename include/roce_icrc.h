@@ -113,7 +113,8 @@ void* ricrc_ctx_stream(ricrc_ctx* ctx);
  *                         the lengths: they follow the context's learned
  *                         hint, which the previous ragged launch's first
  *                         workgroup sets by the same rule from the batch's
- *                         first groups -- so launches enqueued back to back
+ *                         first 12 groups (both kernels probe the same
+ *                         ones) -- so launches enqueued back to back
  *                         follow the last launch FINISHED before them.
  *   RICRC_RAGGED_COMPACT  every ragged launch of the context runs the compact
  *                         kernel.
@@ -127,7 +128,8 @@ int ricrc_ctx_set_ragged_variant(ricrc_ctx* ctx, int variant);
 /* The variant the context's last ragged launch ran (RICRC_RAGGED_COMPACT or
  * RICRC_RAGGED_SORTED; RICRC_RAGGED_SORTED also for the single-width ragged
  * kernels that an explicit lanes setting other than 8 selects),
- * RICRC_RAGGED_AUTO before any. */
+ * RICRC_RAGGED_AUTO before any.  A launch that failed to enqueue does not
+ * change it. */
 int ricrc_ctx_last_ragged_variant(ricrc_ctx* ctx, int* variant_out);
 
 /* ---- host buffers, synchronous (H2D + kernel + D2H) --------------------- */

@@ -237,6 +237,7 @@ def build_frame(
     ttl: int = 64,
     tos: int = 0,
     icrc: int | None = None,
+    ip_options: bytes = b"",
 ) -> bytes:
     """Serialise ``IP(src,dst)/UDP(sport,dport)/BTH/ext/Raw(payload)`` as scapy
     would on emit (src/roce_sq.py:1186-1197, src/roce_rq.py:705-731).
@@ -244,7 +245,14 @@ def build_frame(
     Padding follows src/roce_util.py:187-199: only when a Raw payload is present,
     zero bytes up to a multiple of 4 and BTH.padcount = number of pad bytes.
     The ICRC trailer is computed with ``icrc_of_frame`` unless ``icrc`` is given.
+
+    ``ip_options``: the raw bytes of scapy's ``IP(options=...)`` (the IPv4
+    layer under every emit path, src/roce.py:14-31 imports it); scapy's
+    ``IP.post_build`` zero-pads them to a multiple of 4 and sets
+    ``ihl = header bytes / 4``.
     """
+    opts = bytes(ip_options) + b"\0" * ((-len(ip_options)) % 4)
+    ihl = 5 + len(opts) // 4
     bth = dict(bth)
     body = ext
     if payload is not None:
@@ -254,10 +262,10 @@ def build_frame(
         body = ext + payload + b"\0" * pad
     bth_b = bth_bytes(**bth)
     udp_len = 8 + len(bth_b) + len(body) + 4
-    ip_len = 20 + udp_len
+    ip_len = 4 * ihl + udp_len
     ip_hdr = struct.pack(
-        "!BBHHHBBH4s4s", 0x45, tos, ip_len, ip_id, 0, ttl, 17, 0, ip_aton(src), ip_aton(dst)
-    )
+        "!BBHHHBBH4s4s", 0x40 | ihl, tos, ip_len, ip_id, 0, ttl, 17, 0, ip_aton(src), ip_aton(dst)
+    ) + opts
     ip_hdr = ip_hdr[:10] + struct.pack("!H", inet_checksum(ip_hdr)) + ip_hdr[12:]
     udp_wo = struct.pack("!HHHH", sport, dport, udp_len, 0)
     trailer_placeholder = b"\0\0\0\0"  # FCSField default (src/roce.py:184)

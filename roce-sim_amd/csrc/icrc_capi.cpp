@@ -81,8 +81,10 @@ struct ricrc_ctx {
   struct BatchEv {
     hipStream_t stream;
     hipEvent_t ev;
+    uint64_t seq;  // batch_seq at its last record (slot reuse: the oldest)
   };
   std::vector<BatchEv> batch_evs;
+  uint64_t batch_seq = 0;
   // ragged launches: the host-mapped hint word (tiny_hint) of the context, the
   // caller's variant (RICRC_RAGGED_*) and the one the last launch ran
   uint32_t* tiny_hint = nullptr;
@@ -263,24 +265,36 @@ unsigned long long* claim_region(ricrc_ctx* c, hipStream_t s, uint32_t* epoch) {
 // run undisturbed.
 std::mutex g_batch_mu;
 std::vector<ricrc_ctx*> g_batch_ctxs;  // contexts with batch events
-constexpr size_t kBatchStreams = 16;   // streams tracked per context (the oldest is reused)
+// Streams tracked per context.  A context on more streams reuses a slot whose
+// batch has completed, else the least recently recorded one (its batch is
+// then no longer waited for: at worst a relaunched wave lands beside it,
+// which costs that batch time, never a result).
+constexpr size_t kBatchStreams = 16;
 
 void batch_launched(ricrc_ctx* c, hipStream_t s) {
   if (!device_busy(c->device)) return;  // no service on the device (yet): nothing to hold back
   size_t i = 0;
   while (i < c->batch_evs.size() && c->batch_evs[i].stream != s) ++i;
   if (i == c->batch_evs.size()) {
-    if (i >= kBatchStreams) {  // (a context on very many streams: reuse the first slot)
-      i = 0;
-      c->batch_evs[0].stream = s;
+    if (i >= kBatchStreams) {
+      i = kBatchStreams;
+      for (size_t k = 0; k < c->batch_evs.size() && i == kBatchStreams; ++k)
+        if (hipEventQuery(c->batch_evs[k].ev) == hipSuccess) i = k;
+      if (i == kBatchStreams) {  // every tracked batch still runs: the oldest record
+        i = 0;
+        for (size_t k = 1; k < c->batch_evs.size(); ++k)
+          if (c->batch_evs[k].seq < c->batch_evs[i].seq) i = k;
+      }
+      c->batch_evs[i].stream = s;
     } else {
       hipEvent_t ev = nullptr;
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
       std::lock_guard<std::mutex> lk(g_batch_mu);
       if (c->batch_evs.empty()) g_batch_ctxs.push_back(c);
-      c->batch_evs.push_back({s, ev});
+      c->batch_evs.push_back({s, ev, 0});
     }
   }
+  c->batch_evs[i].seq = ++c->batch_seq;
   (void)hipEventRecord(c->batch_evs[i].ev, s);
 }
 
@@ -417,9 +431,10 @@ int launch(ricrc_ctx* c, const uint8_t* frames, const uint64_t* offs, const uint
                                                                                     : RICRC_RAGGED_SORTED;
       // (automatic lanes, or 8: an explicit other setting keeps its lane groups)
       compact = v == RICRC_RAGGED_COMPACT && (c->lanes == 0 || ricrc::ragged_has_compact(log2g));
-      c->last_ragged = compact ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
     }
     HIP_TRY(ricrc::launch_icrc(a, log2g, ragged, verify, c->num_cus, s, compact));
+    // (only a launch that was enqueued names the variant it ran)
+    if (ragged && n > 0) c->last_ragged = compact ? RICRC_RAGGED_COMPACT : RICRC_RAGGED_SORTED;
   }
   batch_launched(c, s);
   return RICRC_OK;

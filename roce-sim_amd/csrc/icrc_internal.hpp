@@ -9,12 +9,17 @@ namespace ricrc {
 
 // Device table image: 7 main sets (lanes-per-packet G = 1..64, log2 index) of
 // Mul(128 G), then the combine sets: [0] = Mul(-32), [1 + l] = Mul(-128 * 2^l),
-// then Mul(64) (the small-frame kernel's two-chain fold).
+// then Mul(64) (the small-frame kernel's two-chain fold), then Mul(64) once
+// more as the small-frame kernel's LDS rows (Keys8, icrc_device.hpp: row e =
+// 8 copies of entry e of each of the 4 tables, 128 B; the kernel copies the
+// rows into the low halves of its 256-B LDS rows by LDS-DMA).
 constexpr int kMaxLog2G = 6;
 constexpr int kNumMainSets = kMaxLog2G + 1;
 constexpr int kNumCombSets = kMaxLog2G + 1;
 constexpr int kMul64Set = kNumMainSets + kNumCombSets;
-constexpr int kTableWords = (kMul64Set + 1) * 1024;
+constexpr int kSmallImageOff = (kMul64Set + 1) * 1024;  // words
+constexpr int kSmallImageWords = 256 * 32;
+constexpr int kTableWords = kSmallImageOff + kSmallImageWords;
 
 struct IcrcArgs {
   const uint8_t* frames;

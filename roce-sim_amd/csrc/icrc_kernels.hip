@@ -1091,21 +1091,25 @@ __device__ __forceinline__ void mixed_windows(const IcrcArgs& a, int tid, IssueT
 }
 
 // The AUTO hint of the ragged launches (icrc_capi.cpp hint_word): the
-// launch's first workgroup looks at the batch's first 64-packet groups, one
-// per wave (`probe`: the thread's packet length), and stores into the
-// context's host-mapped word whether at least half of them hold only frames
-// of at most kCompactMaxLen bytes -- the compact kernel's candidates.  One
-// store over PCIe per launch (a store per wave made the kernel 2.9x slower,
-// round 4); `scratch`: one LDS word per wave, free at this point.
+// launch's first workgroup looks at the batch's first kHintGroups 64-packet
+// groups, one per wave (`probe`: the thread's packet length, packet tid of the
+// batch, clamped to its last), and stores into the context's host-mapped word
+// whether at least half of them hold only frames of at most kCompactMaxLen
+// bytes -- the compact kernel's candidates.  Both ragged kernels probe the
+// same groups, so the hint depends on the batch, not on which variant ran
+// last.  One store over PCIe per launch (a store per wave made the kernel
+// 2.9x slower, round 4); `scratch`: one LDS word per wave, free at this point.
+constexpr int kHintGroups = 12;
 template <int WAVES>
 __device__ __forceinline__ void store_tiny_hint(uint32_t* hint, uint32_t scratch, int tid, uint32_t probe) {
+  static_assert(WAVES >= kHintGroups, "one probing wave per group");
   if ((tid & 63) == 0) lds_wr(scratch + 4u * (uint32_t)(tid >> 6), __all(probe <= kCompactMaxLen) ? 1u : 0u);
   __syncthreads();
   if (tid == 0) {
     uint32_t tiny = 0;
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) tiny += lds_rd(scratch + 4u * (uint32_t)w);
-    __hip_atomic_store(hint, 2u * tiny >= (uint32_t)WAVES ? 1u : 0u, __ATOMIC_RELAXED,
+    for (int w = 0; w < kHintGroups; ++w) tiny += lds_rd(scratch + 4u * (uint32_t)w);
+    __hip_atomic_store(hint, 2u * tiny >= (uint32_t)kHintGroups ? 1u : 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -1115,10 +1119,7 @@ __device__ __forceinline__ void store_tiny_hint(uint32_t* hint, uint32_t scratch
 template <bool VERIFY>
 __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(IcrcArgs a) {
   const int tid = threadIdx.x;
-  const uint32_t per_block = (a.n + gridDim.x - 1) / gridDim.x;
-  const uint32_t p0 = blockIdx.x * per_block;
-  const uint32_t p1 = min(a.n, p0 + per_block);
-  const uint32_t probe = blockIdx.x == 0 && p0 < p1 ? a.lens[p0 + min((uint32_t)tid, p1 - p0 - 1u)] : 0xFFFFFFFFu;
+  const uint32_t probe = blockIdx.x == 0 && a.n > 0 ? a.lens[min((uint32_t)tid, a.n - 1u)] : 0xFFFFFFFFu;
   announce_batch(a.busy);
   // (uniform) the hint; scratch: the window's sort arrays, not yet in use
   if (a.tiny_hint && blockIdx.x == 0) store_tiny_hint<kIcrcWaves>(a.tiny_hint, MixedLds::kPerm, tid, probe);
@@ -1701,51 +1702,41 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   auto load = [&](uint32_t b) __attribute__((always_inline)) {  // unconditional: clamped batch index
     load_at(a.frames + (uint64_t)min(b, lim) * 64u * S);
   };
-  // The tables: their words are loaded into registers first, then the wave's
-  // first batch goes out (its DMA in flight while the tables are written and
-  // the workgroup meets at the barrier), then vmcnt(C) -- the C younger DMA
-  // loads may still be in flight -- and the LDS writes.  Mul(64) as 8 copies
-  // of 1024 words (2 quads each; >= 512 threads, launch_icrc_small: at most
-  // 4 words per thread), Mul(-32) unreplicated (256 quads).
+  // The tables arrive by LDS-DMA like the batches: no table word passes
+  // through a register, so the compiler has no load of its own to wait for
+  // (it counts no LDS-DMA load: a load of its own would make it wait
+  // vmcnt(0), draining the first batch's DMA too).  Mul(64): the 256 Keys8
+  // rows (128 B each, built on the host, kSmallImageOff) into the low halves
+  // of the 256-B LDS rows -- 64 instructions of 1 KiB of LDS, the lanes whose
+  // 16 bytes fall in a row's high half idle; Mul(-32) unreplicated at
+  // kSmallComb, 4 more.  Instruction j goes to wave j mod nw.  Then the wave's
+  // first batch, then vmcnt(C): the C younger batch loads may still be in
+  // flight, every table load of the wave has landed; then the barrier.
   {
-    const uint32_t* m64 = a.tables + kMul64Set * 1024;       // Mul(32 CH)
-    const uint32_t* cm32 = a.tables + kNumMainSets * 1024;  // combine set 0: Mul(-32)
-    // Loads and LDS writes the compiler cannot see: it does not count the
-    // DMA loads, so it would wait for them too (vmcnt(0)) before the writes.
-    auto ldg_asm = [](const uint32_t* p) {
-      uint32_t v;
-      __asm__ __volatile__("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-      return v;
-    };
-    auto ldg4_asm = [](const uint32_t* p) {
-      u32x4 v;
-      __asm__ __volatile__("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-      return v;
-    };
-    auto ds_wr128 = [](uint32_t addr, u32x4 v) {
-      __asm__ __volatile__("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
-    };
-    constexpr int kTw = 4;
-    uint32_t tw[kTw];
-#pragma unroll
-    for (int k = 0; k < kTw; ++k)  // (unconditional: clamped index)
-      tw[k] = ldg_asm(m64 + (min(tid + k * (int)blockDim.x, 2047) >> 1));
-    const u32x4 cw = ldg4_asm(cm32 + 4 * min(tid, 255));
-    // (no branch around the DMA, or the compiler waits for it with the table
-    // words: a workgroup without staged batches loads a clamped full batch,
-    // or with none in the launch (n <= 64) the table image, and never folds it)
+    const uint8_t* rows = (const uint8_t*)(a.tables + kSmallImageOff);
+    const uint8_t* cm32 = (const uint8_t*)(a.tables + kNumMainSets * 1024);  // combine set 0: Mul(-32)
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(wave);
+#pragma unroll 1
+    for (uint32_t j = wv; j < 68u; j += nw) {  // (uniform)
+      if (j < 64u) {
+        if ((lane & 8) == 0)  // LDS chunk 64 j + lane: row 4 j + lane / 16, its low half
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(rows + 16u * (32u * j + (uint32_t)((lane >> 4) << 3) +
+                                                                            (uint32_t)(lane & 7))),
+              (__attribute__((address_space(3))) void*)(uintptr_t)(1024u * j), 16, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(cm32 + 16u * (64u * (j - 64u) + (uint32_t)lane)),
+            (__attribute__((address_space(3))) void*)(uintptr_t)(kSmallComb + 1024u * (j - 64u)), 16, 0, 0);
+      }
+    }
+    // (no branch around the DMA: a workgroup without staged batches loads a
+    // clamped full batch, or with none in the launch (n <= 64) the table
+    // image, and never folds it)
     load_at(last > 0 ? a.frames + (uint64_t)min(b0 + (uint32_t)wave, lim) * 64u * S
                      : (const uint8_t*)a.tables);
     __asm__ __volatile__("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0x0F70 | C);  // vmcnt(C): the table words are in
-    __asm__ __volatile__("" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < kTw; ++k) {
-      const int i = tid + k * (int)blockDim.x, w = i >> 1, h = i & 1;  // w = t * 256 + e
-      if (i < 2048) ds_wr128((uint32_t)((w & 255) * 256 + (w >> 8) * 32 + h * 16), u32x4{tw[k], tw[k], tw[k], tw[k]});
-    }
-    if (tid < 256) ds_wr128(kSmallComb + 16u * (uint32_t)tid, cw);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the writes are done before the barrier
+    __builtin_amdgcn_s_waitcnt(0x0F70 | C);  // vmcnt(C): the table rows are in LDS
     __asm__ __volatile__("" ::: "memory");
   }
   // (the barrier alone: __syncthreads' fence would wait for the DMA, vmcnt(0))
@@ -2406,7 +2397,12 @@ void build_table_image(uint32_t* out) {
   uint32_t* comb = out + kNumMainSets * 1024;
   table_set(-32, comb);
   for (int l = 0; l < kMaxLog2G; ++l) table_set(-(128ll << l), comb + (1 + l) * 1024);
+  const uint32_t* m64 = out + kMul64Set * 1024;
   table_set(64, out + kMul64Set * 1024);
+  uint32_t* rows = out + kSmallImageOff;  // Keys8 rows of Mul(64), the LDS image's low halves
+  for (int e = 0; e < 256; ++e)
+    for (int t = 0; t < 4; ++t)
+      for (int c = 0; c < 8; ++c) rows[e * 32 + t * 8 + c] = m64[t * 256 + e];
 }
 
 hipError_t set_dynamic_lds(const void* fn, int bytes) {

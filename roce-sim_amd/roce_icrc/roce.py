@@ -232,8 +232,57 @@ def _inet_checksum(data: bytes) -> int:
     return (~s) & 0xFFFF
 
 
+class IPOption:
+    """One IPv4 option as raw bytes (scapy's ``IPOption``: EOL and NOP are a
+    single type byte, every other option type, length, data).  ``bytes()``
+    gives its wire form."""
+
+    def __init__(self, load: bytes = b""):
+        self.load = bytes(load)
+
+    @property
+    def option(self) -> int:
+        return self.load[0] & 0x1F if self.load else 0
+
+    def __bytes__(self):
+        return self.load
+
+    def __eq__(self, other):
+        return isinstance(other, IPOption) and other.load == self.load
+
+    def __repr__(self):
+        return f"<IPOption {self.load.hex()}>"
+
+
+def _split_ip_options(b: bytes) -> list:
+    """Option bytes of a received header into IPOption objects, as scapy's
+    ``PacketListField("options", ..., length_from=ihl*4-20)`` dissects them
+    (a malformed length keeps the rest as one raw option)."""
+    out, i = [], 0
+    while i < len(b):
+        t = b[i]
+        if t in (0, 1):  # EOL, NOP
+            n = 1
+        else:
+            n = b[i + 1] if i + 1 < len(b) else 0
+            if n < 2 or i + n > len(b):
+                n = len(b) - i
+        out.append(IPOption(b[i:i + n]))
+        i += n
+    return out
+
+
 class IP(Packet):
-    """IPv4 with scapy's defaults (ihl/len/proto/chksum computed when None)."""
+    """IPv4 with scapy's defaults (ihl/len/proto/chksum computed when None).
+
+    ``options``: scapy's IPv4 options field (the IP layer the reference's
+    emit wrap stacks under BTH, src/roce.py:14-31, src/roce_sq.py:1189-1193):
+    raw bytes, one ``IPOption`` or a list of them.  As scapy's
+    ``IP.post_build``, the options are zero-padded to a multiple of 4 and
+    ``ihl`` is the header's length in dwords unless given; dissecting a
+    header with ihl > 5 keeps its option bytes (``options``, a list of
+    ``IPOption``).  The ICRC covers them (src/roce.py:202-218 copies the whole
+    IP layer into the pseudo-header)."""
 
     name = "IP"
     fields_desc = [
@@ -242,9 +291,30 @@ class IP(Packet):
         ("chksum", 16, None), ("src", 32, "127.0.0.1"), ("dst", 32, "127.0.0.1"),
     ]
 
+    def __init__(self, _pkt=None, options=None, **kw):
+        super().__init__(None, **kw)
+        self.fields["options"] = [] if options is None else options
+        if _pkt is not None:
+            self.dissect(bytes(_pkt))
+
+    def option_bytes(self) -> bytes:
+        """The options as they go on the wire, zero-padded to whole dwords."""
+        o = self.fields["options"]
+        if isinstance(o, (bytes, bytearray, memoryview)):
+            b = bytes(o)
+        elif isinstance(o, IPOption):
+            b = bytes(o)
+        else:
+            b = b"".join(bytes(x) for x in o)
+        return b + b"\0" * ((-len(b)) % 4)
+
+    def hdr_len(self) -> int:
+        return 20 + len(self.option_bytes())
+
     def _header(self, total_len: int, chksum: Optional[int]) -> bytes:
         f = dict(self.fields)
-        f["ihl"] = 5 if f["ihl"] is None else f["ihl"]
+        opts = self.option_bytes()
+        f["ihl"] = (20 + len(opts)) // 4 if f["ihl"] is None else f["ihl"]
         f["len"] = total_len if f["len"] is None else f["len"]
         if f["proto"] is None:
             f["proto"] = 17 if isinstance(self.payload, UDP) else 0
@@ -254,13 +324,13 @@ class IP(Packet):
         v = 0
         for name, bits, _ in self.fields_desc:
             v = (v << bits) | (int(f[name]) & ((1 << bits) - 1))
-        return v.to_bytes(20, "big")
+        return v.to_bytes(20, "big") + opts
 
     def self_build(self):
         return b""  # built in post_build (needs the payload length)
 
     def post_build(self, p, pay):
-        hdr = self._header(20 + len(pay), self.chksum)
+        hdr = self._header(self.hdr_len() + len(pay), self.chksum)
         if self.chksum is None:
             hdr = hdr[:10] + struct.pack("!H", _inet_checksum(hdr)) + hdr[12:]
         return hdr + pay
@@ -273,6 +343,7 @@ class IP(Packet):
         self.fields["src"] = str(ipaddress.IPv4Address(self.fields["src"]))
         self.fields["dst"] = str(ipaddress.IPv4Address(self.fields["dst"]))
         ihl = self.fields["ihl"]
+        self.fields["options"] = _split_ip_options(bytes(s[20:4 * ihl])) if ihl > 5 else []
         return s[4 * ihl:]
 
     def next_layer(self, rest):
@@ -503,7 +574,7 @@ def wire_frame(ip: IP, udp: UDP, roce: bytes) -> bytes:
     both are ICRC-masked) in front of the built BTH bytes ``roce``."""
     ulen = 8 + len(roce) if udp.len is None else udp.len
     udp_hdr = struct.pack("!HHHH", udp.sport, udp.dport, ulen, udp.chksum or 0)
-    ip_hdr = ip._header(20 + 8 + len(roce), ip.chksum)
+    ip_hdr = ip._header(ip.hdr_len() + 8 + len(roce), ip.chksum)
     return ip_hdr + udp_hdr + roce
 
 

@@ -93,7 +93,8 @@ def uniform_frames(n: int, payload_len: int = 4096, opcode: int = 0x01, seed: in
 
 def shard_frames(n_total: int, rank: int, world: int, payload_len: int = 4096,
                  opcode: int = 0x01, seed: int = SEED_CFG4,
-                 chunk: int = 1 << 14) -> tuple[np.ndarray, int, int, np.ndarray]:
+                 chunk: int = 1 << 14,
+                 out: np.ndarray | None = None) -> tuple[np.ndarray, int, int, np.ndarray]:
     """cfg4: ONE global stream of n_total frames built
     like cfg2 from `seed`, packet i going to rank i mod world; returns this
     rank's shard (packets rank, rank + world, ... in order) as (buffer,
@@ -105,12 +106,19 @@ def shard_frames(n_total: int, rank: int, world: int, payload_len: int = 4096,
     by one bit as ``Generator.integers(0, 2**63 - 1)`` returns them; PSN = i
     mod 2^24), so a rank generates only its own packets: the generator jumps
     over the other ranks' words with ``PCG64.advance``.  At world = 1 the
-    shard is the whole uniform_frames batch, byte for byte."""
+    shard is the whole uniform_frames batch, byte for byte.  ``out``: a
+    uint8 buffer of the shard's size to build it in (e.g. a region of one
+    shared block holding every shard)."""
     assert payload_len % 8 == 0 and 0 <= rank < world
     idx = np.arange(rank, n_total, world, dtype=np.int64)
     n = idx.size
     frame_len = HDR + payload_len + ICRC
-    buf = np.empty(n * frame_len, dtype=np.uint8)
+    if out is None:
+        buf = np.empty(n * frame_len, dtype=np.uint8)
+    else:
+        buf = out.reshape(-1)
+        if buf.dtype != np.uint8 or buf.size != n * frame_len:
+            raise ValueError(f"out must be {n * frame_len} uint8 bytes")
     rows = buf.reshape(n, frame_len)
     tmpl = header_template(payload_len, opcode)
     W = payload_len // 8

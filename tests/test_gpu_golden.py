@@ -42,6 +42,27 @@ def test_bth_post_build_through_engine(engine):
     assert frame[-4:] == bytes.fromhex("751de21b")
 
 
+def test_ipv4_options_post_build_and_emit_batch(engine):
+    """IP(options=...) frames (ihl 6..15) through the engine: BTH.post_build
+    (src/roce.py:228-233) and emit_batch give the oracle's frame byte for
+    byte, the ICRC over the longer header included; they verify on the GPU."""
+    R.set_engine(engine)
+    pkts, refs = [], []
+    for i, raw in enumerate([b"\x01\x01\x01\x00", b"\x94\x04\x00\x00", b"\x07\x07\x04\x0a\x0b\x0c\x0d",
+                             b"\x01" * 40, b"\x83\x0b\x04" + bytes(8)]):
+        payload = bytes((i + k) & 0xFF for k in range(13 + 50 * i))
+        refs.append(o.build_frame("10.0.0.1", "10.0.0.2", 0x21, dict(opcode=0x0A, psn=i, dqpn=0x21),
+                                  ext=o.reth_bytes(i, 7, len(payload)), payload=payload, ip_options=raw))
+        b = R.add_padding_if_needed(R.BTH(opcode=0x0A, psn=i, dqpn=0x21) /
+                                    R.RETH(va=i, rkey=7, dlen=len(payload)) / R.Raw(load=payload))
+        pkts.append(R.IP(src="10.0.0.1", dst="10.0.0.2", options=raw) / R.UDP(dport=4791, sport=0x21) / b)
+    assert [bytes(p) for p in pkts] == refs  # one by one: post_build -> ricrc_compute_one
+    assert R.emit_batch(pkts) == refs  # one GPU call
+    assert R.verify_frames(refs).all()
+    got, dropped = R.recv_datagrams(refs)
+    assert dropped == [] and [b.psn for b in got] == list(range(5))
+
+
 def test_emit_batch_and_verify(engine):
     R.set_engine(engine)
     rng = np.random.default_rng(1)

@@ -284,3 +284,24 @@ def test_bench_multi_rank_cfg4_rehearsal_full_size(tmp_path):
     agg = N * cov / (line["ms_per_step"] * 1e-3) / 2**30
     assert abs(line["value"] - agg) < 0.01 * line["value"]
     assert min(line["per_rank_GiBps"]) * N <= line["value"] * 1.01
+
+
+@pytest.mark.timeout(600)
+def test_cfg4_stated_size_one_process():
+    """BASELINE config 4 at its stated size through the HIP path without an
+    8-rank launch (scripts/cfg4_one_process.py): the eight shards
+    synth.shard_frames(2^23, r, 8) of the one 0x1C2C0004 stream, all resident
+    on device 0 together, each through the rank's ricrc_compute_strided_dev,
+    every one of the 2^23 words against the C oracle; then the same host
+    stream split round robin by ricrc_compute_batch_multi over eight contexts
+    on device 0, bit-exact (src/roce.py:192-219: per-packet independence)."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    import cfg4_one_process as c4
+    res = c4.run(23, 8)
+    out_dir = ROOT / "gpurun_out"
+    out_dir.mkdir(exist_ok=True)
+    (out_dir / "cfg4_one_process.json").write_text(json.dumps(res) + "\n")
+    assert res["packets_total"] == 1 << 23 and res["packets_per_shard"] == 1 << 20
+    assert res["resident"]["mismatches_per_shard"] == [0] * 8, res
+    assert res["multi"]["mismatches"] == 0, res
+    assert res["pass"]

@@ -74,6 +74,39 @@ def test_dissect_roundtrip_and_bindings():
         assert R._BTH_BINDINGS.get(op, R.Raw) is cls
 
 
+@pytest.mark.parametrize("opts", [
+    b"\x01\x01\x01\x00",                      # NOP NOP NOP EOL (ihl 6)
+    [R.IPOption(b"\x94\x04\x00\x00")],        # router alert (ihl 6)
+    [R.IPOption(b"\x07\x07\x04"), R.IPOption(b"\x0a\x0b\x0c\x0d")],  # record route, zero pad
+    b"\x01" * 40,                              # the largest header (ihl 15)
+])
+def test_ipv4_options_build_and_dissect(opts):
+    """IP(options=...) under the RoCE stack (scapy's IP layer, src/roce.py:14-31;
+    the emit wrap src/roce_sq.py:1189-1193): ihl > 5, options zero-padded to
+    whole dwords, lengths and checksums over the longer header -- byte for
+    byte the oracle's restatement -- and dissect keeps the option bytes."""
+    raw = opts if isinstance(opts, bytes) else b"".join(bytes(x) for x in opts)
+    payload = bytes(range(37))
+    ref = o.build_frame("10.1.1.48", "10.1.1.15", 9, dict(opcode=0x0A, psn=5, dqpn=0x77),
+                        ext=o.reth_bytes(0x1000, 0x22, 37), payload=payload, ip_options=raw)
+    ihl = 5 + (len(raw) + 3) // 4
+    assert ref[0] == 0x40 | ihl and len(ref) == 4 * ihl + 8 + 12 + 16 + 40 + 4
+    pkt = R.add_padding_if_needed(
+        R.BTH(opcode=0x0A, psn=5, dqpn=0x77) / R.RETH(va=0x1000, rkey=0x22, dlen=37) / R.Raw(load=payload))
+    l3 = R.IP(src="10.1.1.48", dst="10.1.1.15", options=opts) / R.UDP(dport=4791, sport=9) / pkt
+    l3[R.BTH].__dict__["icrc"] = struct.unpack("!I", ref[-4:])[0]
+    assert bytes(l3) == ref
+    assert struct.unpack("<I", ref[-4:])[0] == o.icrc_of_frame(ref) == o.icrc_bitwise(ref)
+    d = R.IP(ref)
+    assert d.ihl == ihl and b"".join(bytes(x) for x in d.options) == ref[20:4 * ihl]
+    assert d[R.UDP].dport == 4791 and d[R.BTH].psn == 5 and d[R.RETH].dlen == 37
+    assert d[R.Raw].load == payload + b"\0\0\0"
+    assert bytes(d) == ref  # round trip: the dissected packet rebuilds the same frame
+    # the wire frame compute_icrc hands the engine is the frame with a zero slot
+    assert R.wire_frame(l3, l3[R.UDP], bytes(l3[R.BTH])[:-4] + b"\0" * 4)[:4 * ihl] == \
+        ref[:10] + bytes(2) + ref[12:4 * ihl]
+
+
 def test_opcode_table_and_cnp():
     assert R.opcode("RC", "SEND_ONLY") == (0x04, "RC_SEND_ONLY")
     assert R.opcode("XRC", "FETCH_ADD")[0] == 0xB4
