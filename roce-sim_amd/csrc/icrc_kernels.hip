@@ -1144,7 +1144,8 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // window barriers and no sort.
 //
 // A wave takes 64-packet groups of its workgroup's contiguous range
-// (round-robin over the workgroup's waves).  Per group: the lanes' 12-byte
+// (round-robin over the workgroup's waves: one group per turn, or with the
+// output ring below kCompactTurn consecutive groups per turn).  Per group: the lanes' 12-byte
 // descriptors, then the compact test of phase 0 (every live frame 44-128 B,
 // dword-aligned, in order without overlap, inside 4 KiB from the first
 // frame's 16-byte line); a compact group's span arrives with four coalesced
@@ -1162,6 +1163,25 @@ __global__ void __launch_bounds__(kIcrcThreads, 1) icrc_ragged_mixed_kernel(Icrc
 // (the list's capacity).
 // Twelve waves (A/B, round 5: 16 waves, or three span buffers per wave, ran
 // 2-4 % slower; at 16 waves the pipeline and the fallback's registers spill).
+// Output words of compute launches (icrc_out, no verify): each wave holds 16
+// rounds of words in registers and writes them back to back, and takes its
+// groups 8 consecutive ones per turn, so a flush covers two contiguous 2-KiB
+// runs.  The 4-byte words written into the saturating read stream cost far
+// more than their bytes: the ACK kernel without its stores ran 0.1545-0.1573
+// ms against 0.1817-0.1836 (words to an L2-resident window: the same 0.155,
+// so the cost is HBM writes, not the store instructions; round 6,
+// profiles/r06/ab_r06b.txt, ab_r06c.txt).  2^24 ACK frames, 3 A/B rounds
+// (ab_r06c, ab_r06d): one store per group (nt) 0.1817-0.1836 ms; ring 16
+// 0.1741-0.1749; ring 16 + 16-group turns 0.1679-0.1685, with sc1 stores
+// 0.1665-0.1682, nt sc1 0.1667-0.1673, default policy 0.1743-0.1749; ring 16
+// + 8-group turns + sc1 0.1659-0.1671 (kept); ring 8 + 8-group turns + sc1
+// 0.1706-0.1721; ring 32 + 32-group turns 0.1797-0.1839 (168 VGPRs); 16-group
+// turns without the ring 0.1904-0.1910 (hence one-group turns when there is
+// no ring: verify launches and compute launches without icrc_out).
+constexpr int kCompactRing = 16;    // rounds held (a power of two)
+constexpr int kCompactTurn = 8;     // consecutive groups per wave per turn (with the ring)
+constexpr int kCompactRingPol = 16;  // sc1
+typedef uint32_t compact_ring_t __attribute__((ext_vector_type(kCompactRing)));
 constexpr int kCompactWaves = 12;
 // Chains per frame: two over Mul(64) (the small-frame kernel's set), one
 // Mul(-32) combine step: ACK kernel 0.1930 -> 0.1865 ms over 4 A/B rounds
@@ -1250,6 +1270,7 @@ __device__ __forceinline__ void compact_fallback_group(const IcrcArgs& a, uint32
 
 template <bool VERIFY, int OUTS>  // OUTS: 1 = icrc_out, 2 = status_out present
 __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcArgs a) {
+  constexpr bool RING = (OUTS & 1) != 0 && !VERIFY;  // icrc_out words through the register ring
   const int tid = threadIdx.x;
   announce_batch(a.busy);
   // Mul(1024) in the rows' low halves with the combine sets and fix-up LUT
@@ -1283,11 +1304,31 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
   for (uint32_t c0 = g0; c0 < g1; c0 += kCompactChunk, ++chunk) {
     const uint32_t c1 = min(g1, c0 + kCompactChunk);
     lds_u32* const nd = ndef + (chunk & 1u);
-    // this wave's groups of the chunk: c0 + wave + kCompactWaves i, i < cnt
-    const uint32_t first = c0 + (uint32_t)wave;
-    const int cnt = first < c1 ? (int)((c1 - first + kCompactWaves - 1) / kCompactWaves) : 0;
-    auto group = [&](int i) { return first + (uint32_t)i * kCompactWaves; };
+    // this wave's groups of the chunk: turns of kCompactWaves * K groups, the
+    // wave's K consecutive ones in each, i < cnt
+    constexpr uint32_t K = RING ? (uint32_t)kCompactTurn : 1u, TURN = kCompactWaves * K;
+    const uint32_t ng = c1 - c0, nturn = ng / TURN, rem = ng - nturn * TURN;
+    const uint32_t mine = rem > (uint32_t)wave * K ? min(K, rem - (uint32_t)wave * K) : 0u;
+    const int cnt = (int)(nturn * K + mine);
+    auto group = [&](int i) {
+      return c0 + (uint32_t)i / K * TURN + (uint32_t)wave * K + (uint32_t)i % K;
+    };
     if (cnt > 0) {  // (uniform)
+      compact_ring_t wr = {};
+      uint32_t held = 0;  // (uniform) ring slots holding a compact group's words
+      // the ring's rounds [base, base + count) to icrc_out, back to back
+      auto flush = [&](int base, int count) __attribute__((always_inline)) {
+        if constexpr (RING) {
+#pragma unroll
+          for (int r = 0; r < kCompactRing; ++r) {
+            if (r < count && ((held >> r) & 1u)) {  // (uniform)
+              const uint32_t pk = group(base + r) * 64u + (uint32_t)lane;
+              if (pk < a.n) stg32<kCompactRingPol>(a.icrc_out + pk, wr[r]);
+            }
+          }
+          held = 0;
+        }
+      };
       // descriptors of the wave's group i (clamped: unconditional loads)
       auto load_desc = [&](int i, uint32_t& L, uint64_t& off) __attribute__((always_inline)) {
         const uint32_t gi = group(min(i, cnt - 1));
@@ -1413,8 +1454,12 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
             if (good && !ok) st |= kPktIcrcMismatch;
             stg8<kCompactStorePol>(a.ok_out + pkt, ok ? 1u : 0u);
           }
-          if constexpr ((OUTS & 1) != 0) stg32<kCompactStorePol>(a.icrc_out + pkt, icrc);
+          if constexpr ((OUTS & 1) != 0 && !RING) stg32<kCompactStorePol>(a.icrc_out + pkt, icrc);
           if constexpr ((OUTS & 2) != 0) stg8<kCompactStorePol>(a.status_out + pkt, st);
+        }
+        if constexpr (RING) {
+          wr[i & (kCompactRing - 1)] = icrc;
+          held |= 1u << (i & (kCompactRing - 1));
         }
         __asm__ __volatile__("" ::: "memory");
       };
@@ -1457,6 +1502,7 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
         issue(c, X);
         body_prio_lo();
         run(i, cur);
+        if (RING && (i & (kCompactRing - 1)) == kCompactRing - 1) flush(i - (kCompactRing - 1), kCompactRing);
       };
       int i = 0;
       for (; i + 1 < cnt; i += 2) {
@@ -1464,6 +1510,7 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
         step(i + 1, cb, XB, Lb, ob, La, oa);
       }
       if (i < cnt) step(i, ca, XA, La, oa, Lb, ob);
+      if (RING && (cnt & (kCompactRing - 1)) != 0) flush(cnt & ~(kCompactRing - 1), cnt & (kCompactRing - 1));
     }  // (cnt > 0)
     // the chunk's listed groups, by every wave of the workgroup; the other
     // counter is free until the next chunk
