@@ -1362,8 +1362,25 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
         const uint32_t L = c.L;  // (dead lanes repeat the last live frame)
         const uint32_t pb = slot + c.rel;
         const int n = (int)((L - 4u) >> 2);  // (10 .. 31: the test checked every lane)
-        const uint32_t d0 = lds_rd(pb), d2 = lds_rd(pb + 8);
-        const uint32_t trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
+        // frames of 48 or 64 B on 16-byte slot boundaries, one length (packed
+        // ACK runs): read as 16-byte quads (conflict-free at a 48-B stride,
+        // where dword reads are 4-way)
+        u32x4 q[4];
+        uint32_t d0, d2, trailer;
+        const uint32_t L0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)L);
+        const bool quads = __all((pb & 15u) == 0 && L == L0 && (L0 == 48u || L0 == 64u));
+        if (quads) {  // (uniform)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (t < 3 || L0 == 64u) q[t] = *(const lds_u32x4*)(uintptr_t)(pb + 16u * (uint32_t)t);
+          d0 = q[0].x;
+          d2 = q[0].z;
+          trailer = VERIFY ? (L0 == 64u ? q[3].w : q[2].w) : 0u;
+        } else {
+          d0 = lds_rd(pb);
+          d2 = lds_rd(pb + 8);
+          trailer = VERIFY ? lds_rd(pb + 4u * (uint32_t)n) : 0u;
+        }
         uint32_t st = 0;
         const int ihl = (int)(d0 & 0xFu);
         if (((d0 >> 4) & 0xFu) != 4u || ihl < 5)
@@ -1381,8 +1398,9 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
         // frames just start later); PAD < 0: per-lane pads, frames patched in
         // place; else every frame of the group has the same length, its masks
         // and seed applied in registers (dwords 0 and 2 are d0 and d2)
-        auto fold = [&](auto padc, int ns, uint32_t pz, int pad) __attribute__((always_inline)) {
+        auto fold = [&](auto padc, int ns, uint32_t pz, int pad, auto qc) __attribute__((always_inline)) {
           constexpr int PAD = decltype(padc)::value;
+          constexpr bool Q = decltype(qc)::value;  // dwords from q[] (one length, PAD 1)
           uint32_t P[CH], T[CH];
 #pragma unroll
           for (int cc = 0; cc < CH; ++cc) P[cc] = T[cc] = 0;
@@ -1398,12 +1416,14 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
                   w = kp >= pad ? w : 0u;
                 } else {
                   const int k = kp - PAD;  // (a constant after unrolling)
-                  if (k < 0)
-                    w = 0u;
-                  else if (k == 0)
+                  // a zero absorbed into a zero register leaves it zero
+                  if (k < 0) continue;
+                  if (k == 0)
                     w = (d0 | 0x0000FF00u) ^ kSeedRegister;
                   else if (k == 2)
                     w = d2 | 0xFFFF00FFu;
+                  else if constexpr (Q)
+                    w = q[(k >> 2) & 3][k & 3];
                   else
                     w = lds_rd(pz + 4u * (uint32_t)kp);
                   if (k == 6) w |= 0xFFFF0000u;
@@ -1422,10 +1442,12 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
         if (__all(good && ihl == 5 && n == n0)) {  // (uniform) one length
           const int ns = (n0 + CH - 1) / CH, pad = CH * ns - n0;
           static_assert(CH == 2, "one instantiation per pad");
-          if (pad == 0)
-            R = fold(std::integral_constant<int, 0>{}, ns, pb, 0);
+          if (quads)  // (48 or 64 B: pad 1)
+            R = fold(std::integral_constant<int, 1>{}, ns, pb - 4u, 1, std::true_type{});
+          else if (pad == 0)
+            R = fold(std::integral_constant<int, 0>{}, ns, pb, 0, std::false_type{});
           else
-            R = fold(std::integral_constant<int, 1>{}, ns, pb - 4u, 1);
+            R = fold(std::integral_constant<int, 1>{}, ns, pb - 4u, 1, std::false_type{});
         } else if (__all(good && ihl == 5)) {
           // masks and seed patched in place (every lane reads its dwords before
           // any writes them: a dead lane's copy of the last frame writes the same
@@ -1443,7 +1465,7 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
           }
           const int ns = __builtin_amdgcn_readfirstlane(nsm);
           const int pad = CH * ns - n;
-          R = fold(std::integral_constant<int, -1>{}, ns, pb - 4u * (uint32_t)pad, pad);
+          R = fold(std::integral_constant<int, -1>{}, ns, pb - 4u * (uint32_t)pad, pad, std::false_type{});
         } else {
           R = fold_masked4<false, MixedKeysS, kComb, kCompactChains>(nullptr, pb, ihl, n);
         }
@@ -1466,10 +1488,10 @@ __global__ void __launch_bounds__(kCompactThreads, 1) icrc_compact_kernel(IcrcAr
       // write a group's span registers into the slot (the slot's previous group
       // is folded: LDS ops of a wave run in issue order)
       auto stage = [&](const CGroup& c, const u32x4 (&X)[kCompactLoads]) __attribute__((always_inline)) {
-        const uint32_t last = (c.span + 15u) / 16u - 1u;
+        // (unclamped: the slot holds all 256 chunks; the chunks past the span
+        // repeat its last one and are never read)
 #pragma unroll
-        for (int t = 0; t < kCompactLoads; ++t)
-          *(lds_u32x4*)(uintptr_t)(slot + 16u * min((uint32_t)(lane + 64 * t), last)) = X[t];
+        for (int t = 0; t < kCompactLoads; ++t) *(lds_u32x4*)(uintptr_t)(slot + 16u * (uint32_t)(lane + 64 * t)) = X[t];
         __asm__ __volatile__("" ::: "memory");
       };
 
@@ -1789,6 +1811,21 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
   // (the barrier alone: __syncthreads' fence would wait for the DMA, vmcnt(0))
   __builtin_amdgcn_s_barrier();
   __asm__ __volatile__("" ::: "memory");
+  // The last batch, straight from global memory (one wave of the owning
+  // block): its per-dword loads and dependent fold run first, under the other
+  // waves' streams, not at the end of the launch (cfg5 0.2906-0.2925 ->
+  // 0.2880-0.2921 ms, 4 A/B rounds, profiles/r06/ab_r06p.txt).
+  {
+    if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % nw) {
+      const uint32_t pkt = last * 64u + (uint32_t)lane;
+      const bool live = pkt < a.n;
+      const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
+      int ihl;
+      const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
+      const uint32_t R = small_fold_masked_global<SmallKeys, kSmallComb, CH>(f, ihl, n);
+      emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
+    }
+  }
   // One batch: the slot's batch has landed; the wave reads its frames into
   // registers and at once refills the slot with the next batch (in flight
   // during the fold, its loads at raised wave priority), then checks the
@@ -1934,16 +1971,6 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves, 1) icrc_small_kernel(Icrc
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA outlives its slot's use
-  // the last batch, straight from global memory (one wave of the owning block)
-  if (last >= b0 && last < b1 && (uint32_t)wave == (last - b0) % nw) {
-    const uint32_t pkt = last * 64u + (uint32_t)lane;
-    const bool live = pkt < a.n;
-    const uint8_t* f = a.frames + (uint64_t)(live ? pkt : a.n - 1) * S;
-    int ihl;
-    const uint32_t st = check(ldg32(f), ldg32(f + 8), ihl);
-    const uint32_t R = small_fold_masked_global<SmallKeys, kSmallComb, CH>(f, ihl, n);
-    emit(pkt, live, st, R, VERIFY ? ldg32(f + 4 * n) : 0u);
-  }
 }
 
 // STREAM-style read ceiling: one workgroup per CU sweeping a contiguous
