@@ -416,3 +416,34 @@ def test_compact_kernel_second_chunk_of_a_workgroup(engine):
     expect = np.ones(n, bool)
     expect[flipped] = False
     np.testing.assert_array_equal(ok, expect)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 64 * 12 * 8 - 1, 64 * 12 * 8 + 1, 64 * 12 * 16 * 3 + 100,
+                               64 * 256 * 12 * 8 + 5 * 64 + 3])
+def test_compact_output_ring_edges(engine, n):
+    """The compact kernel's output ring (round 6: 16 rounds of words per wave in
+    registers, 8-group turns, flushed back to back): batches whose group count
+    leaves partial turns, partial rings and a last partial group, with and
+    without status bytes (icrc only: the ring; icrc + status: the ring and
+    per-group status stores), against the oracle."""
+    torch = pytest.importorskip("torch")
+    buf, offs, lens = _ack_stream(n, n)
+    want, _ = oracle_batch(buf, offs, lens)
+    d = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    engine.set_ragged_variant(E.RAGGED_COMPACT)
+    try:
+        for with_status in (False, True):
+            out = torch.full((n + 64,), -1, dtype=torch.int32, device="cuda")
+            st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda") if with_status else None
+            engine.compute_batch_dev(d, do, dl, n, out, st)
+            assert engine.last_ragged_variant() == E.RAGGED_COMPACT
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint32)
+            np.testing.assert_array_equal(got[:n], want, err_msg=f"status {with_status}")
+            assert (got[n:] == 0xFFFFFFFF).all(), "a word was written past the batch"
+            if with_status:
+                assert not st.cpu().numpy().any()
+    finally:
+        engine.set_ragged_variant(E.RAGGED_AUTO)
