@@ -82,25 +82,77 @@ __global__ void __launch_bounds__(1024) stream_copy(const u32x4* __restrict__ s,
   for (; i < n16; i += stride) d[i] = s[i];
 }
 
+// One event pair around `reps` launches (a pair per launch drains each
+// launch's writes at the release, round 5), mean ms per launch.
 template <class F>
-static float time_it(F f, int reps = 10) {
+static float time_it(F f, int reps = 20) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   for (int i = 0; i < 3; ++i) f();
   CK(hipDeviceSynchronize());
-  std::vector<float> t;
-  for (int i = 0; i < reps; ++i) {
-    CK(hipEventRecord(a));
-    f();
-    CK(hipEventRecord(b));
-    CK(hipEventSynchronize(b));
-    float ms;
-    CK(hipEventElapsedTime(&ms, a, b));
-    t.push_back(ms);
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+// Round 6: one packet per wave at a time, streamed: a wave owns a contiguous
+// range of packets and walks its (packet, 1-KiB chunk) sequence with loads U
+// chunks ahead across packet boundaries (no per-set restart); chunk j of
+// packet p: lane i reads MR bytes 1024 j + 16 i - hdr of the packet (clamped
+// into the packet) and writes slot bytes 1024 j + 16 i while < the frame
+// rounded up to 128 B.
+template <int U, int W>
+__global__ void __launch_bounds__(64 * W, 1) segstream(const uint8_t* mr, uint8_t* out, uint32_t n, int kHdr,
+                                                          int kFrame, uint32_t kSlot) {
+  const int lane = threadIdx.x & 63;
+  const int C = (kFrame + 1023) / 1024;          // chunks per packet
+  const int fr = (kFrame + 127) & ~127;          // bytes written per packet
+  const uint32_t nw = gridDim.x * W;
+  const uint32_t wid = blockIdx.x * W + (threadIdx.x >> 6);
+  const uint32_t per = (n + nw - 1) / nw;
+  const uint32_t p0 = wid * per, p1 = min(n, p0 + per);
+  if (p0 >= p1) return;
+  const uint32_t T = (p1 - p0) * C;
+  auto ld = [&](uint32_t t) -> u32x4 {
+    t = min(t, T - 1);
+    const uint32_t p = p0 + t / C, j = t % C;
+    int o = 1024 * (int)j + 16 * lane - kHdr;
+    o = max(0, min(o, (int)kMsg - 16));
+    return *(const u32x4_u*)(mr + (uint64_t)p * kMsg + o);
+  };
+  u32x4 R[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) R[u] = ld(u);
+  for (uint32_t t = 0; t < T; t += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t tt = t + u;
+      const u32x4 v = R[u];
+      R[u] = ld(tt + U);
+      if (tt < T) {
+        const uint32_t p = p0 + tt / C, j = tt % C;
+        const int o = 1024 * (int)j + 16 * lane;
+        if (o < fr) __builtin_nontemporal_store(v, (u32x4*)(out + (uint64_t)p * kSlot + o));
+      }
+    }
   }
-  std::sort(t.begin(), t.end());
-  return t[t.size() / 2];
+}
+
+template <int U, int W>
+static void run_stream(const uint8_t* mr, uint8_t* out, uint32_t n, int cus, int hdr, int frame, uint32_t slot) {
+  auto go = [&] { hipLaunchKernelGGL((segstream<U, W>), dim3(cus), dim3(64 * W), 0, 0, mr, out, n, hdr, frame, slot); };
+  go();
+  CK(hipGetLastError());
+  const float ms = time_it(go);
+  const double bytes = (double)n * kMsg + (double)n * frame;
+  printf("{\"kernel\": \"segstream\", \"hdr\": %d, \"frame\": %d, \"slot\": %u, \"U\": %d, \"waves\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
+         hdr, frame, slot, U, W, ms, bytes / ms / 1e6);
+  fflush(stdout);
 }
 
 template <int LOG2G, int U, int W, int POL>
@@ -124,14 +176,19 @@ int main() {
   CK(hipMemset(mr, 0x5A, (size_t)n * kMsg));
   CK(hipMemset(out, 0, (size_t)n * 4352));
   const uint64_t n16 = (uint64_t)n * kMsg / 16;
-  const float sc = time_it([&] { hipLaunchKernelGGL(stream_copy, dim3(cus * 8), dim3(1024), 0, 0, (const u32x4*)mr, (u32x4*)out, n16); });
+  const float sc = time_it([&] { hipLaunchKernelGGL(stream_copy, dim3(cus), dim3(1024), 0, 0, (const u32x4*)mr, (u32x4*)out, n16); });
   printf("{\"kernel\": \"stream_copy\", \"ms\": %.4f, \"GBps\": %.1f}\n", sc, 2.0 * n16 * 16 / sc / 1e6);
-  const int geo[][3] = {{40, 4140, 4352}, {0, 4096, 4096}, {40, 4140, 4224}, {0, 4096, 4352}, {40, 4140, 4140},
-                       {0, 4096, 4224}, {40, 4096, 4096}};
-  for (auto& g : geo) {
-    run<3, 4, 8, 2>(mr, out, n, cus, g[0], g[1], (uint32_t)g[2]);
-    run<3, 4, 16, 2>(mr, out, n, cus, g[0], g[1], (uint32_t)g[2]);
-    run<5, 4, 16, 2>(mr, out, n, cus, g[0], g[1], (uint32_t)g[2]);
+  // round 6: loads in flight per lane (U) x waves per CU at the shipped
+  // geometry (40-B header, 4140-B frames, 4224-B slots), 3 rounds
+  for (int r = 0; r < 3; ++r) {
+    run<3, 4, 8, 2>(mr, out, n, cus, 40, 4140, 4224);
+    run<3, 4, 8, 2>(mr, out, n, cus, 0, 4096, 4096);
+    run_stream<4, 8>(mr, out, n, cus, 40, 4140, 4224);
+    run_stream<8, 8>(mr, out, n, cus, 40, 4140, 4224);
+    run_stream<4, 16>(mr, out, n, cus, 40, 4140, 4224);
+    run_stream<8, 16>(mr, out, n, cus, 40, 4140, 4224);
+    run_stream<4, 8>(mr, out, n, cus, 0, 4096, 4096);
+    run_stream<8, 16>(mr, out, n, cus, 0, 4096, 4096);
   }
   CK(hipFree(mr));
   CK(hipFree(out));
