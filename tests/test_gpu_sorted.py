@@ -110,3 +110,56 @@ def test_sorted_offsets_beyond_2_34(engine):
         engine.set_ragged_variant(E.RAGGED_AUTO)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
     del big
+
+
+# Workgroup-range shapes (round 6, written for byte-balanced ranges, which
+# were measured slower and not kept: scratch/attic/sorted_byte_balance_r06.diff,
+# DESIGN.md section 12): ranges of very unequal bytes, offsets out of order in
+# places, repeated frames, descending offsets.  Every packet must be covered
+# exactly once: every word and every verdict byte is checked.
+
+def test_balanced_ranges_skewed_lengths(engine):
+    """Buffer-order frames, the first 40 % of 4 KiB MTU, the rest 256-B
+    payloads: workgroup ranges of very unequal bytes."""
+    n = 1 << 20
+    k = n * 2 // 5
+    b1, o1, l1 = synth.mixed_mtu_frames(k, mtus=(4096,), seed=31)
+    b2, o2, l2 = synth.mixed_mtu_frames(n - k, mtus=(256,), seed=32)
+    buf = np.concatenate([b1, b2])
+    offs = np.concatenate([o1, o2 + np.uint64(b1.size)])
+    lens = np.concatenate([l1, l2])
+    want, _ = oracle_batch(buf, offs, lens)
+    got, st = _sorted_run(engine, buf, offs, lens, flip_every=997, status=True)
+    np.testing.assert_array_equal(got, want)
+    assert not st.any()
+
+
+def test_balanced_ranges_local_swaps_and_duplicates(engine):
+    """Buffer order broken by scattered swaps of neighbours, and runs of
+    descriptors that repeat one frame (equal offsets)."""
+    rng = np.random.default_rng(41)
+    n = 600011
+    buf, offs, lens = synth.mixed_mtu_frames(n, seed=42)
+    offs, lens = offs.copy(), lens.copy()
+    for i in rng.choice(n - 1, 700, replace=False):
+        offs[[i, i + 1]] = offs[[i + 1, i]]
+        lens[[i, i + 1]] = lens[[i + 1, i]]
+    for i in rng.choice(n - 8, 300, replace=False):
+        offs[i:i + 4] = offs[i]
+        lens[i:i + 4] = lens[i]
+    want, _ = oracle_batch(buf, offs, lens)
+    got, _ = _sorted_run(engine, buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("n", [256 * 1024 + 5, 400009])
+def test_balanced_ranges_descending_and_short_ranges(engine, n):
+    """Offsets in ascending and in descending order, ~1024-1600 packets per
+    workgroup."""
+    buf, offs, lens = synth.mixed_mtu_frames(n, seed=n + 1)
+    want, _ = oracle_batch(buf, offs, lens)
+    got, _ = _sorted_run(engine, buf, offs, lens, flip_every=313)
+    np.testing.assert_array_equal(got, want)
+    r = np.arange(n)[::-1]
+    got, _ = _sorted_run(engine, buf, offs[r].copy(), lens[r].copy(), flip_every=313)
+    np.testing.assert_array_equal(got, want[r])
